@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident rANS encode+decode on MI355X (BASELINE.json metric).
+
+A "step" is one pass of the hot path over one batch: encode every chunk of the
+synthetic iid symbol array (one reference Message per chunk, IID<Categorical>::push,
+src/codec.rs:415-420) and decode it back (IID::pop, src/codec.rs:422-424).
+
+Default workload = SURVEY.md §8d config C3 (BASELINE.json configs[2]): 2^30 u8 symbols,
+256-symbol table (norm 139,224,331), chunk_len 4096, generated on the device by the
+counter-based splitmix64 generator (so every rank's shard is a slice of one global
+array).  With --gpus N (torchrun, one process per GPU) each rank codes its own 2^30
+symbol shard (weak scaling, no collective on the data path).
+
+value = total uncompressed symbol GiB of all ranks / (max-over-ranks time per step).
+roofline: algorithmic bytes of the dominant kernel (n*w symbols + compressed stream
+bytes) / its average launch time from HIP events on its stream.
+cpu_baseline: the oracle (oracle/ans_oracle.c, single thread) timed on a bounded
+sample of the same workload (rank 0, N=1 only).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "shuffle-coding_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import ans_amd as A  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+CONFIGS = {
+    # name: (masses fn, log2 n per rank, symbol bytes, seed)
+    "c3": (A.c3_masses, 30, 1, 1),
+    "c4": (A.c4_masses, 29, 2, 2),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--log2n", type=int, default=None, help="symbols per rank = 2^log2n (default: the config's)")
+    p.add_argument("--chunk-len", type=int, default=4096)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def lib_hash():
+    h = hashlib.sha256()
+    with open(A.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel_key, n_launch_bytes_hint):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of THIS library build
+    (profiles/pmc_<libhash>.json, written by tools/pmc_summary.py), else None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{lib_hash()}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel_key)
+    return None if k is None else k.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(masses, sym_bytes, seed, chunk_len, target_s):
+    """Oracle (single thread) encode+decode on the first chunks of the same workload."""
+    from oracle import oracle as orc
+    pilot = 64 * chunk_len
+    syms = orc.gen_iid(masses, seed, 0, pilot)
+    t0 = time.perf_counter()
+    d, o, l = orc.encode_chunks(masses, syms, chunk_len)
+    orc.decode_chunks(masses, d, o, l, pilot, chunk_len)
+    per_sym = (time.perf_counter() - t0) / pilot
+    nchunks = max(64, int(target_s / per_sym / chunk_len))
+    n = nchunks * chunk_len
+    syms = orc.gen_iid(masses, seed, 0, n)
+    t0 = time.perf_counter()
+    d, o, l = orc.encode_chunks(masses, syms, chunk_len)
+    t1 = time.perf_counter()
+    back = orc.decode_chunks(masses, d, o, l, n, chunk_len)
+    t2 = time.perf_counter()
+    assert np.array_equal(back, syms)
+    return {
+        "value": n * sym_bytes / (t2 - t0) / 2**30,
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {nchunks} chunks x {chunk_len} symbols ({n} symbols) of the same workload; "
+                  f"encode {t1 - t0:.2f}s + decode {t2 - t1:.2f}s, oracle/ans_oracle.c single thread",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    masses_fn, log2n, sym_bytes, seed = CONFIGS[args.config]
+    if args.log2n is not None:
+        log2n = args.log2n
+    n = 1 << log2n
+    L = args.chunk_len
+    nchunks = -(-n // L)
+    masses = masses_fn()
+
+    gpu = A.Gpu(local)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    cap = gt.slot_capacity(L)
+    stream = torch.cuda.current_stream()
+    dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
+    syms = torch.empty(n, dtype=dt, device="cuda")
+    gt.dev_gen_iid(seed, rank * n, n, syms, sym_bytes, stream)  # this rank's slice of the global array
+    slots = torch.empty(nchunks * cap, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty_like(syms)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        gt.dev_encode(syms, sym_bytes, n, L, slots, cap, lens, status, stream)
+        if ev is not None:
+            ev[1].record(stream)
+        gt.dev_decode(slots, None, cap, lens, n, L, out, sym_bytes, status, stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    # ---- verification (outside the timed region)
+    st = gpu.status(status, stream)
+    if st != 0:
+        raise SystemExit(f"device status {st}: {A.lib().ans_status_string(st).decode()}")
+    if not torch.equal(out, syms):
+        raise SystemExit("round trip failed: decoded symbols differ")
+    comp_bytes = int(lens.to(torch.int64).sum().item())
+
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    total_sym_bytes = world * n * sym_bytes
+    value = total_sym_bytes / (elapsed / args.steps) / 2**30
+
+    alg_bytes = n * sym_bytes + comp_bytes  # per launch, encode and decode alike
+    dom_name, dom_ms = ("decode", dec_ms) if dec_ms >= enc_ms else ("encode", enc_ms)
+    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(f"k_{dom_name}", alg_bytes)
+
+    if rank == 0:
+        line = {
+            "metric": "ANS encode+decode GiB/s (device-resident) at 1/2/4/8 MI355X; % HBM roofline",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (counter-based splitmix64 iid symbols generated on device, SURVEY.md §8d)",
+            "config": {
+                "workload": f"{args.config.upper()}: 2^{log2n} iid u{8 * sym_bytes} symbols per GPU, "
+                            f"{len(masses)}-symbol Categorical (norm {int(masses.sum())}), chunk_len {L}",
+                "symbols_per_gpu": n,
+                "symbol_bytes": sym_bytes,
+                "chunk_len": L,
+                "chunks_per_gpu": nchunks,
+                "parallelism": f"chunk-sharded x{world}, no collective",
+            },
+            "encode_ms": round(enc_ms, 4),
+            "decode_ms": round(dec_ms, 4),
+            "encode_gib_s": round(n * sym_bytes / (enc_ms * 1e-3) / 2**30, 3),
+            "decode_gib_s": round(n * sym_bytes / (dec_ms * 1e-3) / 2**30, 3),
+            "compressed_bytes_per_symbol": round(comp_bytes / n, 5),
+            "parity": "round trip verified on device; byte parity: tests/test_gpu_parity.py",
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"k_{dom_name}",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(masses, sym_bytes, seed, L, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

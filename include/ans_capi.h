@@ -1,0 +1,164 @@
+/*
+ * ans_capi.h — C ABI of the MI355X-native rANS coder (libshufflecoding_amd.so).
+ *
+ * This is the drop-in boundary for the reference's ANS hot path
+ * (entropy-coding/shuffle-coding @ 2024_08_07).  Plain pointers and sizes only; no
+ * exceptions cross it; caller-owned buffers; no pointer is retained after a call
+ * returns (handles excepted).  Every entry point names the reference interface it
+ * replaces.  A Rust caller binds it with an `extern "C"` block.
+ *
+ * Threading: a Message handle is single-threaded (the reference's `&mut Message`);
+ * tables are immutable after creation and may be shared; GPU handles are per device,
+ * one HIP stream each, and must not be used from two threads at once.
+ */
+#ifndef ANS_CAPI_H
+#define ANS_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (the reference panics; we return these instead) ---- */
+#define ANS_OK 0
+#define ANS_E_ZERO_MASS 1   /* src/ans.rs:98     assert_ne!(p, 0)                        */
+#define ANS_E_EXHAUSTED 2   /* src/ans.rs:144    "Message exhausted whilst attempting decode." */
+#define ANS_E_LEN 3         /* src/codec.rs:416  IID length assert / output buffer too small  */
+#define ANS_E_SYMBOL 4      /* src/codec.rs:63   symbol index out of range                */
+#define ANS_E_NORM_RANGE 5  /* src/codec.rs:35   size/norm outside what the coder supports */
+#define ANS_E_DEVICE 6      /* HIP runtime error or no GPU                                */
+#define ANS_E_ALLOC 7       /* host or device allocation failed                           */
+#define ANS_E_ARG 8         /* invalid argument (NULL handle, bad width, ...)             */
+#define ANS_E_MISMATCH 9    /* a reference property check failed (src/ans.rs:52-57)       */
+
+/* ---- tail generators: src/ans.rs:131-136 TailGenerator ---- */
+#define ANS_GEN_ZEROS 0  /* Message::zeros()  src/ans.rs:292 */
+#define ANS_GEN_EMPTY 1  /* Message::empty()  src/ans.rs:297 */
+#define ANS_GEN_RANDOM 2 /* Message::random() src/ans.rs:285 (host only; bytes parity-unpinned) */
+
+const char *ans_status_string(int status);
+int ans_abi_version(void); /* bumps on any incompatible change */
+
+/* ======================================================================
+ * (1) Message handle — replaces `pub struct Message { head, tail }`
+ *     (src/ans.rs:225-310).
+ * ====================================================================== */
+typedef struct ans_msg ans_msg;
+
+/* Message::zeros()/empty()/random(seed)  src/ans.rs:285-299 */
+int ans_msg_new(int gen_kind, uint64_t seed, ans_msg **out);
+void ans_msg_free(ans_msg *m);
+/* Clone  (#[derive(Clone)] src/ans.rs:225) */
+int ans_msg_clone(const ans_msg *m, ans_msg **out);
+/* m.clone().flatten().elements  src/ans.rs:255-260.  *len receives the byte count;
+ * with out == NULL or cap < *len nothing is copied (size query / ANS_E_LEN). */
+int ans_msg_flatten(const ans_msg *m, uint8_t *out, size_t cap, size_t *len);
+/* Message::unflatten(Tail::new(bytes, generator))  src/ans.rs:262-264 */
+int ans_msg_unflatten(const uint8_t *bytes, size_t len, int gen_kind, uint64_t seed, ans_msg **out);
+/* Message::unflatten(m.clone().flatten()) keeping the Tail's generator state and
+ * num_generated, as the reference's round-trip check does (src/ans.rs:57) */
+int ans_msg_reflatten(const ans_msg *m, ans_msg **out);
+/* Message::bits / virtual_bits  src/ans.rs:267-283 */
+int ans_msg_bits(const ans_msg *m, uint64_t *bits);
+int ans_msg_virtual_bits(const ans_msg *m, double *bits);
+/* PartialEq for Message (canonicalising)  src/ans.rs:302-310 */
+int ans_msg_equal(const ans_msg *a, const ans_msg *b, int *equal);
+/* field access: m.head, m.tail.elements.len(), m.tail.num_generated */
+int ans_msg_state(const ans_msg *m, uint64_t *head, uint64_t *tail_len, uint64_t *num_generated);
+
+/* ======================================================================
+ * (2) Two-phase scalar op — replaces the blanket `impl<D: Distribution> Codec for D`
+ *     (src/ans.rs:93-121) for ANY Distribution, including ones whose cdf depends on i
+ *     (e.g. PlainOrbitCodec, src/recursive/plain_orbit.rs:33-49).
+ *       push: ans_push_begin(m, pmf(x), norm, &q, &r); c = cdf(x, r); ans_push_end(m, norm, q, c)
+ *       pop:  ans_pop_begin(m, norm, &q, &cf); (x, r) = icdf(cf); ans_pop_end(m, pmf(x), q, r)
+ * ====================================================================== */
+int ans_push_begin(ans_msg *m, uint64_t p, uint64_t norm, uint64_t *q, uint64_t *r); /* ans.rs:97-102 */
+int ans_push_end(ans_msg *m, uint64_t norm, uint64_t q, uint64_t cdf);               /* ans.rs:103-104 */
+int ans_pop_begin(ans_msg *m, uint64_t norm, uint64_t *q, uint64_t *cf);             /* ans.rs:108-111 */
+int ans_pop_end(ans_msg *m, uint64_t p, uint64_t q, uint64_t r);                     /* ans.rs:112-114 */
+/* Uniform::push/pop  src/codec.rs:18-31 (size <= MAX_SIZE = 2^46, src/ans.rs:22) */
+int ans_uniform_push(ans_msg *m, uint64_t size, uint64_t x);
+int ans_uniform_pop(ans_msg *m, uint64_t size, uint64_t *x);
+
+/* ======================================================================
+ * (3) Static tables — replaces `Categorical` / `Bernoulli` (src/codec.rs:51-129) and
+ *     `IID<Categorical>` on ONE message (src/codec.rs:405-443), on the host.
+ * ====================================================================== */
+typedef struct ans_table ans_table;
+
+/* Categorical::new(masses)  src/codec.rs:72-80 */
+int ans_table_create(const uint64_t *masses, uint32_t nsym, ans_table **out);
+/* Bernoulli::new(mass, norm) = Categorical[norm-mass, mass]  src/codec.rs:125-128 */
+int ans_table_create_bernoulli(uint64_t mass, uint64_t norm, ans_table **out);
+void ans_table_free(ans_table *t);
+int ans_table_info(const ans_table *t, uint32_t *nsym, uint64_t *norm);
+/* Categorical as a Codec (blanket impl)  src/ans.rs:96-116 */
+int ans_cat_push(ans_msg *m, const ans_table *t, uint64_t x);
+int ans_cat_pop(ans_msg *m, const ans_table *t, uint64_t *x);
+/* IID::push (reverse order) / IID::pop (forward)  src/codec.rs:415-424 */
+int ans_push_iid(ans_msg *m, const ans_table *t, const uint32_t *syms, size_t n);
+int ans_pop_iid(ans_msg *m, const ans_table *t, uint32_t *out, size_t n);
+
+/* ======================================================================
+ * (4) GPU bulk path (MI355X / gfx950) — the data-parallel hot path.
+ *     n symbols are cut into chunks of chunk_len (the last may be shorter); chunk j is
+ *     ONE independent reference message: Message::zeros(), IID<Categorical>::push of
+ *     its symbols (src/codec.rs:415-420, src/ans.rs:96-105), flatten (src/ans.rs:255).
+ *     Its stream is byte-identical to that.  Decode is IID::pop on
+ *     Message::unflatten(stream) (src/codec.rs:422-424, src/ans.rs:107-116,262).
+ *     Symbols are unsigned integers of sym_bytes = 1, 2 or 4 bytes.
+ *     Supported tables: 1 <= nsym <= 65536 and norm < 2^32 (ANS_E_NORM_RANGE otherwise).
+ * ====================================================================== */
+typedef struct ans_gpu ans_gpu;
+typedef struct ans_gpu_table ans_gpu_table;
+
+int ans_gpu_device_count(int *count);
+/* one context per device; owns a HIP stream */
+int ans_gpu_create(int device, ans_gpu **out);
+void ans_gpu_free(ans_gpu *g);
+/* uploads the table (and its derived reciprocal / icdf-bucket data) to the device */
+int ans_gpu_table_create(ans_gpu *g, const ans_table *t, ans_gpu_table **out);
+void ans_gpu_table_free(ans_gpu_table *gt);
+/* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
+int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);
+
+/* Host buffers in, host buffers out (synchronous; includes H2D/D2H).
+ * Encode writes the streams densely: chunk j at out[offsets[j] .. offsets[j]+lens[j]).
+ * out_cap must hold the total (query the exact total by passing out == NULL: *total is
+ * set and nothing else is written). */
+int ans_gpu_encode_chunks(ans_gpu_table *gt, const void *syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                          uint8_t *out, uint64_t out_cap, uint64_t *offsets, uint64_t *lens, uint64_t *total);
+/* gen_kind = ANS_GEN_ZEROS or ANS_GEN_EMPTY (what an exhausted stream yields); returns
+ * ANS_E_MISMATCH if a chunk does not return to Message::zeros() (src/ans.rs:56). */
+int ans_gpu_decode_chunks(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
+                          const uint64_t *lens, uint64_t n, uint64_t chunk_len, int gen_kind, void *out,
+                          int sym_bytes);
+
+/* Device-resident variants: all pointers are device pointers; asynchronous on `stream`
+ * (a hipStream_t; NULL = the context's stream).  Streams live in fixed slots: chunk j at
+ * d_slots + j*slot_cap (slot_cap from ans_gpu_slot_capacity).  Errors found on the
+ * device are OR-ed into *d_status as (1u << status) bits; read with ans_dev_status. */
+int ans_dev_encode_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                          uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status, void *stream);
+/* d_offsets == NULL: chunk j's stream starts at d_in + j*slot_cap (the encoder's layout);
+ * otherwise at d_in + d_offsets[j] (e.g. a dense container). */
+int ans_dev_decode_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
+                          const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void *d_syms,
+                          int sym_bytes, uint32_t *d_status, void *stream);
+/* Synthetic iid symbols, counter-based: symbol i of seed k is
+ * icdf(floor(splitmix64((k << 48) ^ (start + i)) * norm / 2^64)). */
+int ans_dev_gen_iid(ans_gpu_table *gt, uint64_t seed, uint64_t start, uint64_t n, void *d_syms, int sym_bytes,
+                    void *stream);
+/* Compacts slot streams into a dense buffer: d_out[d_offsets[j] ..] = slot j. */
+int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const uint32_t *d_lens,
+                    const uint64_t *d_offsets, uint64_t nchunks, uint8_t *d_out, void *stream);
+/* Synchronises `stream` and maps the device status word to the lowest set status. */
+int ans_dev_status(ans_gpu *g, const uint32_t *d_status, void *stream, int *status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ANS_CAPI_H */

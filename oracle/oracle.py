@@ -1,0 +1,227 @@
+"""ctypes wrapper around oracle/build/libans_oracle.so (the C restatement).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — as the checker, never as the product path.
+See oracle/ans_oracle.c for what it restates (src/ans.rs, src/codec.rs).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libans_oracle.so")
+
+ZEROS, EMPTY, RANDOM = 0, 1, 2
+_lib = None
+
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+vp = ctypes.c_void_p
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        sigs = {
+            "orc_msg_new": (vp, [ctypes.c_int, u64]),
+            "orc_msg_free": (None, [vp]),
+            "orc_msg_clone": (vp, [vp]),
+            "orc_msg_err": (ctypes.c_int, [vp]),
+            "orc_msg_head": (u64, [vp]),
+            "orc_msg_tail_len": (u64, [vp]),
+            "orc_msg_num_generated": (u64, [vp]),
+            "orc_msg_flatten": (u64, [vp, vp, u64]),
+            "orc_msg_unflatten": (vp, [vp, u64, ctypes.c_int, u64]),
+            "orc_msg_reflatten": (vp, [vp]),
+            "orc_msg_bits": (u64, [vp]),
+            "orc_msg_virtual_bits": (ctypes.c_double, [vp]),
+            "orc_msg_equal": (ctypes.c_int, [vp, vp]),
+            "orc_cat_new": (vp, [vp, u32]),
+            "orc_cat_free": (None, [vp]),
+            "orc_cat_norm": (u64, [vp]),
+            "orc_cat_push": (ctypes.c_int, [vp, vp, u64]),
+            "orc_cat_pop": (ctypes.c_int, [vp, vp, ctypes.POINTER(u64)]),
+            "orc_uniform_push": (ctypes.c_int, [vp, u64, u64]),
+            "orc_uniform_pop": (ctypes.c_int, [vp, u64, ctypes.POINTER(u64)]),
+            "orc_iid_push": (ctypes.c_int, [vp, vp, vp, u64]),
+            "orc_iid_pop": (ctypes.c_int, [vp, vp, vp, u64]),
+            "orc_encode_chunks": (ctypes.c_int, [vp, u32, vp, u64, u64, ctypes.c_int, u64, vp, u64, vp, vp]),
+            "orc_decode_chunks": (ctypes.c_int, [vp, u32, vp, vp, vp, u64, u64, ctypes.c_int, u64, vp]),
+            "orc_gen_iid": (ctypes.c_int, [vp, u32, u64, u64, u64, vp]),
+            "orc_splitmix64": (u64, [u64]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Message:
+    """Mirror of the reference `Message` (src/ans.rs:225-310) backed by the C oracle."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def zeros(cls):
+        return cls(lib().orc_msg_new(ZEROS, 0))
+
+    @classmethod
+    def empty(cls):
+        return cls(lib().orc_msg_new(EMPTY, 0))
+
+    @classmethod
+    def random(cls, seed):
+        return cls(lib().orc_msg_new(RANDOM, seed))
+
+    @classmethod
+    def unflatten(cls, data, kind=ZEROS, seed=0):
+        buf = np.frombuffer(bytes(data), dtype=np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
+        return cls(lib().orc_msg_unflatten(_ptr(buf), len(data), kind, seed))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_msg_free(self.h)
+            self.h = None
+
+    def clone(self):
+        return Message(lib().orc_msg_clone(self.h))
+
+    @property
+    def head(self):
+        return lib().orc_msg_head(self.h)
+
+    @property
+    def err(self):
+        return lib().orc_msg_err(self.h)
+
+    @property
+    def num_generated(self):
+        return lib().orc_msg_num_generated(self.h)
+
+    def flatten(self):
+        n = lib().orc_msg_flatten(self.h, None, 0)
+        buf = np.zeros(max(n, 1), np.uint8)
+        lib().orc_msg_flatten(self.h, _ptr(buf), n)
+        return bytes(buf[:n])
+
+    def reflatten(self):
+        return Message(lib().orc_msg_reflatten(self.h))
+
+    def bits(self):
+        return lib().orc_msg_bits(self.h)
+
+    def virtual_bits(self):
+        return lib().orc_msg_virtual_bits(self.h)
+
+    def __eq__(self, other):
+        return bool(lib().orc_msg_equal(self.h, other.h))
+
+
+class Categorical:
+    """Mirror of `Categorical` (src/codec.rs:51-92) backed by the C oracle."""
+
+    def __init__(self, masses):
+        self.masses = np.ascontiguousarray(np.asarray(masses, dtype=np.uint64))
+        self.h = lib().orc_cat_new(_ptr(self.masses), len(self.masses))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_cat_free(self.h)
+            self.h = None
+
+    @property
+    def norm(self):
+        return lib().orc_cat_norm(self.h)
+
+    def push(self, m, x):
+        return lib().orc_cat_push(m.h, self.h, int(x))
+
+    def pop(self, m):
+        x = u64(0)
+        rc = lib().orc_cat_pop(m.h, self.h, ctypes.byref(x))
+        if rc:
+            raise RuntimeError(f"oracle pop failed rc={rc}")
+        return x.value
+
+    def push_iid(self, m, syms):
+        s = np.ascontiguousarray(np.asarray(syms, dtype=np.uint32))
+        return lib().orc_iid_push(m.h, self.h, _ptr(s), len(s))
+
+    def pop_iid(self, m, n):
+        out = np.zeros(max(n, 1), np.uint32)
+        rc = lib().orc_iid_pop(m.h, self.h, _ptr(out), n)
+        if rc:
+            raise RuntimeError(f"oracle iid pop failed rc={rc}")
+        return out[:n]
+
+
+def uniform_push(m, size, x):
+    return lib().orc_uniform_push(m.h, size, x)
+
+
+def uniform_pop(m, size):
+    x = u64(0)
+    rc = lib().orc_uniform_pop(m.h, size, ctypes.byref(x))
+    if rc:
+        raise RuntimeError(f"oracle uniform pop failed rc={rc}")
+    return x.value
+
+
+def encode_chunks(masses, syms, chunk_len, kind=ZEROS, seed=0):
+    """Returns (dense stream bytes as np.uint8, offsets u64, lens u64)."""
+    masses = np.ascontiguousarray(np.asarray(masses, dtype=np.uint64))
+    syms = np.ascontiguousarray(np.asarray(syms, dtype=np.uint32))
+    n = len(syms)
+    nchunks = (n + chunk_len - 1) // chunk_len
+    cap = 6 * n + 16 * nchunks + 16
+    out = np.zeros(cap, np.uint8)
+    offsets = np.zeros(max(nchunks, 1), np.uint64)
+    lens = np.zeros(max(nchunks, 1), np.uint64)
+    rc = lib().orc_encode_chunks(_ptr(masses), len(masses), _ptr(syms), n, chunk_len, kind, seed,
+                                 _ptr(out), cap, _ptr(offsets), _ptr(lens))
+    if rc:
+        raise RuntimeError(f"oracle encode failed rc={rc}")
+    total = int(lens[:nchunks].sum())
+    return out[:total].copy(), offsets[:nchunks].copy(), lens[:nchunks].copy()
+
+
+def decode_chunks(masses, data, offsets, lens, n, chunk_len, kind=ZEROS, seed=0):
+    masses = np.ascontiguousarray(np.asarray(masses, dtype=np.uint64))
+    data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+    if data.size == 0:
+        data = np.zeros(1, np.uint8)
+    offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+    lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    out = np.zeros(max(n, 1), np.uint32)
+    rc = lib().orc_decode_chunks(_ptr(masses), len(masses), _ptr(data), _ptr(offsets), _ptr(lens), n,
+                                 chunk_len, kind, seed, _ptr(out))
+    if rc:
+        raise RuntimeError(f"oracle decode failed rc={rc}")
+    return out[:n]
+
+
+def gen_iid(masses, seed, start, n):
+    masses = np.ascontiguousarray(np.asarray(masses, dtype=np.uint64))
+    out = np.zeros(max(n, 1), np.uint32)
+    lib().orc_gen_iid(_ptr(masses), len(masses), seed, start, n, _ptr(out))
+    return out[:n]
+
+
+def splitmix64(x):
+    return lib().orc_splitmix64(x)

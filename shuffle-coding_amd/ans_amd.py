@@ -1,0 +1,599 @@
+"""Python binding of libshufflecoding_amd.so (include/ans_capi.h) via ctypes.
+
+Mirrors the reference's coder surface with the same names and argument meaning:
+  Message.zeros/empty/random/unflatten, flatten, bits, virtual_bits, ==   src/ans.rs:225-310
+  Codec.push/pop/bits/sample/samples, test_invertibility/test             src/ans.rs:28-75
+  Distribution (norm/pmf/cdf/icdf) through the two-phase scalar ABI       src/ans.rs:80-121
+  Uniform / Categorical / Bernoulli / IID / Independent                   src/codec.rs
+and exposes the GPU bulk path (section 4 of the header): GpuTable.encode_chunks /
+decode_chunks on host buffers and dev_encode / dev_decode / dev_gen_iid on device
+memory (torch tensors or raw pointers).
+
+There is no CPU fallback for the GPU path: if the shared library or the GPU is missing,
+the calls raise.
+"""
+import collections
+import ctypes
+import math
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libshufflecoding_amd.so")
+
+ANS_OK, ANS_E_ZERO_MASS, ANS_E_EXHAUSTED, ANS_E_LEN, ANS_E_SYMBOL = 0, 1, 2, 3, 4
+ANS_E_NORM_RANGE, ANS_E_DEVICE, ANS_E_ALLOC, ANS_E_ARG, ANS_E_MISMATCH = 5, 6, 7, 8, 9
+GEN_ZEROS, GEN_EMPTY, GEN_RANDOM = 0, 1, 2
+MAX_MIN_HEAD = 1 << 56
+MAX_SIZE = MAX_MIN_HEAD >> 10
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+u64 = ctypes.c_uint64
+sz = ctypes.c_size_t
+ci = ctypes.c_int
+
+# name -> (restype, argtypes); this list is also the ABI-export test's expectation.
+SIGNATURES = {
+    "ans_status_string": (ctypes.c_char_p, [ci]),
+    "ans_abi_version": (ci, []),
+    "ans_msg_new": (ci, [ci, u64, ctypes.POINTER(vp)]),
+    "ans_msg_free": (None, [vp]),
+    "ans_msg_clone": (ci, [vp, ctypes.POINTER(vp)]),
+    "ans_msg_flatten": (ci, [vp, vp, sz, ctypes.POINTER(sz)]),
+    "ans_msg_unflatten": (ci, [vp, sz, ci, u64, ctypes.POINTER(vp)]),
+    "ans_msg_reflatten": (ci, [vp, ctypes.POINTER(vp)]),
+    "ans_msg_bits": (ci, [vp, u64p]),
+    "ans_msg_virtual_bits": (ci, [vp, ctypes.POINTER(ctypes.c_double)]),
+    "ans_msg_equal": (ci, [vp, vp, ctypes.POINTER(ci)]),
+    "ans_msg_state": (ci, [vp, u64p, u64p, u64p]),
+    "ans_push_begin": (ci, [vp, u64, u64, u64p, u64p]),
+    "ans_push_end": (ci, [vp, u64, u64, u64]),
+    "ans_pop_begin": (ci, [vp, u64, u64p, u64p]),
+    "ans_pop_end": (ci, [vp, u64, u64, u64]),
+    "ans_uniform_push": (ci, [vp, u64, u64]),
+    "ans_uniform_pop": (ci, [vp, u64, u64p]),
+    "ans_table_create": (ci, [vp, ctypes.c_uint32, ctypes.POINTER(vp)]),
+    "ans_table_create_bernoulli": (ci, [u64, u64, ctypes.POINTER(vp)]),
+    "ans_table_free": (None, [vp]),
+    "ans_table_info": (ci, [vp, u32p, u64p]),
+    "ans_cat_push": (ci, [vp, vp, u64]),
+    "ans_cat_pop": (ci, [vp, vp, u64p]),
+    "ans_push_iid": (ci, [vp, vp, vp, sz]),
+    "ans_pop_iid": (ci, [vp, vp, vp, sz]),
+    "ans_gpu_device_count": (ci, [ctypes.POINTER(ci)]),
+    "ans_gpu_create": (ci, [ci, ctypes.POINTER(vp)]),
+    "ans_gpu_free": (None, [vp]),
+    "ans_gpu_table_create": (ci, [vp, vp, ctypes.POINTER(vp)]),
+    "ans_gpu_table_free": (None, [vp]),
+    "ans_gpu_slot_capacity": (ci, [vp, u64, u64p]),
+    "ans_gpu_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_decode_chunks": (ci, [vp, vp, u64, vp, vp, u64, u64, ci, vp, ci]),
+    "ans_dev_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_decode_chunks": (ci, [vp, vp, vp, u64, vp, u64, u64, ci, vp, ci, vp, vp]),
+    "ans_dev_gen_iid": (ci, [vp, u64, u64, u64, vp, ci, vp]),
+    "ans_dev_compact": (ci, [vp, vp, u64, vp, vp, u64, vp, vp]),
+    "ans_dev_status": (ci, [vp, vp, vp, ctypes.POINTER(ci)]),
+}
+
+_lib = None
+
+
+class AnsError(RuntimeError):
+    def __init__(self, code, where=""):
+        self.code = code
+        msg = lib().ans_status_string(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{where}: {msg} (status {code})" if where else f"{msg} (status {code})")
+
+
+def lib():
+    """Loads the in-tree shared library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `make -C shuffle-coding_amd` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, where=""):
+    if rc != ANS_OK:
+        raise AnsError(rc, where)
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(vp)
+
+
+# ============================================================== Message (src/ans.rs:225-310)
+class Message:
+    __slots__ = ("h",)
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def _new(cls, kind, seed=0):
+        h = vp()
+        _check(lib().ans_msg_new(kind, seed, ctypes.byref(h)), "Message::new")
+        return cls(h)
+
+    @classmethod
+    def zeros(cls):
+        return cls._new(GEN_ZEROS)
+
+    @classmethod
+    def empty(cls):
+        return cls._new(GEN_EMPTY)
+
+    @classmethod
+    def random(cls, seed):
+        return cls._new(GEN_RANDOM, seed)
+
+    @classmethod
+    def unflatten(cls, data, kind=GEN_ZEROS, seed=0):
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        h = vp()
+        _check(lib().ans_msg_unflatten(_np_ptr(buf) if len(buf) else None, len(buf), kind, seed, ctypes.byref(h)),
+               "Message::unflatten")
+        return cls(h)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            _lib.ans_msg_free(h)
+            self.h = None
+
+    def clone(self):
+        h = vp()
+        _check(lib().ans_msg_clone(self.h, ctypes.byref(h)), "Message::clone")
+        return Message(h)
+
+    def flatten(self):
+        n = sz(0)
+        _check(lib().ans_msg_flatten(self.h, None, 0, ctypes.byref(n)), "Message::flatten")
+        buf = np.zeros(max(n.value, 1), np.uint8)
+        _check(lib().ans_msg_flatten(self.h, _np_ptr(buf), n.value, ctypes.byref(n)), "Message::flatten")
+        return bytes(buf[:n.value])
+
+    def reflatten(self):
+        """Message::unflatten(self.clone().flatten()) with the tail's generator kept (src/ans.rs:57)."""
+        h = vp()
+        _check(lib().ans_msg_reflatten(self.h, ctypes.byref(h)), "Message::unflatten(flatten)")
+        return Message(h)
+
+    def bits(self):
+        b = u64(0)
+        _check(lib().ans_msg_bits(self.h, ctypes.byref(b)), "Message::bits")
+        return b.value
+
+    def virtual_bits(self):
+        b = ctypes.c_double(0)
+        _check(lib().ans_msg_virtual_bits(self.h, ctypes.byref(b)), "Message::virtual_bits")
+        return b.value
+
+    def state(self):
+        h, t, g = u64(0), u64(0), u64(0)
+        _check(lib().ans_msg_state(self.h, ctypes.byref(h), ctypes.byref(t), ctypes.byref(g)))
+        return h.value, t.value, g.value
+
+    @property
+    def head(self):
+        return self.state()[0]
+
+    def __eq__(self, other):
+        e = ci(0)
+        _check(lib().ans_msg_equal(self.h, other.h, ctypes.byref(e)), "Message::eq")
+        return bool(e.value)
+
+    def __ne__(self, other):
+        return not self == other
+
+
+# ============================================================== Codec trait (src/ans.rs:28-75)
+CodecTestResults = collections.namedtuple("CodecTestResults", "bits amortized_bits enc_sec dec_sec")
+
+
+def assert_bits_close(expected_bits, bits, tol):  # src/ans.rs:329-332
+    mismatch = abs(bits - expected_bits) / max(abs(expected_bits), 1.0)
+    assert mismatch < tol, f"Expected {expected_bits} bits, but got {bits} bits."
+
+
+def assert_bits_eq(expected_bits, bits):  # src/ans.rs:325-327
+    assert_bits_close(expected_bits, bits, 1e-5)
+
+
+class Codec:
+    def push(self, m, x):
+        raise NotImplementedError
+
+    def pop(self, m):
+        raise NotImplementedError
+
+    def bits(self, x):
+        return None
+
+    def sample(self, seed):  # src/ans.rs:38-40
+        return self.pop(Message.random(seed))
+
+    def samples(self, length, seed):  # src/ans.rs:42-44
+        return IID(self, length).sample(seed)
+
+    def test_invertibility(self, x, initial):  # src/ans.rs:47-59
+        import time
+        m = initial.clone()
+        t0 = time.perf_counter()
+        self.push(m, x)
+        enc_sec = time.perf_counter() - t0
+        bits = m.bits()
+        amortized_bits = m.virtual_bits() - initial.virtual_bits()
+        assert bits >= amortized_bits
+        t0 = time.perf_counter()
+        decoded = self.pop(m)
+        dec_sec = time.perf_counter() - t0
+        assert _sym_eq(x, decoded), "decoded != x"
+        assert initial == m, "message did not return to its initial state"
+        assert initial == m.reflatten(), "flatten/unflatten round trip"
+        return CodecTestResults(bits, amortized_bits, enc_sec, dec_sec)
+
+    def test(self, x, initial):  # src/ans.rs:62-68
+        out = self.test_invertibility(x, initial)
+        b = self.bits(x)
+        if b is not None:
+            assert_bits_eq(b, out.amortized_bits)
+        return out
+
+    def test_on_samples(self, num_samples):  # src/ans.rs:72-74
+        return [self.test(self.sample(seed), Message.random(seed)).amortized_bits for seed in range(num_samples)]
+
+
+def _sym_eq(a, b):
+    if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+        return np.array_equal(np.asarray(a), np.asarray(b))
+    return a == b
+
+
+class Distribution(Codec):
+    """A Python Distribution (norm/pmf/cdf/icdf) coded through the two-phase scalar ABI,
+    exactly as the blanket `impl<D: Distribution> Codec for D` (src/ans.rs:93-121)."""
+
+    def norm(self):
+        raise NotImplementedError
+
+    def pmf(self, x):
+        raise NotImplementedError
+
+    def cdf(self, x, i):
+        raise NotImplementedError
+
+    def icdf(self, cf):
+        raise NotImplementedError
+
+    def push(self, m, x):
+        q, r = u64(0), u64(0)
+        _check(lib().ans_push_begin(m.h, self.pmf(x), self.norm(), ctypes.byref(q), ctypes.byref(r)), "push")
+        _check(lib().ans_push_end(m.h, self.norm(), q.value, self.cdf(x, r.value)), "push")
+
+    def pop(self, m):
+        q, cf = u64(0), u64(0)
+        _check(lib().ans_pop_begin(m.h, self.norm(), ctypes.byref(q), ctypes.byref(cf)), "pop")
+        x, r = self.icdf(cf.value)
+        _check(lib().ans_pop_end(m.h, self.pmf(x), q.value, r), "pop")
+        return x
+
+    def bits(self, x):  # src/ans.rs:118-120
+        return math.log2(self.norm()) - math.log2(self.pmf(x))
+
+
+class Uniform(Distribution):  # src/codec.rs:13-49
+    def __init__(self, size):
+        assert size <= MAX_SIZE
+        self.size = size
+
+    def norm(self):
+        return self.size
+
+    def pmf(self, x):
+        return 1
+
+    def cdf(self, x, i):
+        assert i == 0
+        return x
+
+    def icdf(self, cf):
+        return cf, 0
+
+    def push(self, m, x):
+        _check(lib().ans_uniform_push(m.h, self.size, x), "Uniform::push")
+
+    def pop(self, m):
+        x = u64(0)
+        _check(lib().ans_uniform_pop(m.h, self.size, ctypes.byref(x)), "Uniform::pop")
+        return x.value
+
+    def uni_bits(self):
+        return math.log2(self.size)
+
+
+class Categorical(Distribution):  # src/codec.rs:51-92
+    def __init__(self, masses):
+        self.masses = np.ascontiguousarray(np.asarray(masses, dtype=np.uint64))
+        self.cummasses = np.concatenate([[0], np.cumsum(self.masses)[:-1]]).astype(np.uint64) if len(
+            self.masses) else np.zeros(0, np.uint64)
+        self._norm = int(self.masses.sum()) if len(self.masses) else 0
+        h = vp()
+        _check(lib().ans_table_create(_np_ptr(self.masses), len(self.masses), ctypes.byref(h)), "Categorical::new")
+        self.table = h
+
+    def __del__(self):
+        h = getattr(self, "table", None)
+        if h and _lib is not None:
+            _lib.ans_table_free(h)
+            self.table = None
+
+    def norm(self):
+        return self._norm
+
+    def pmf(self, x):
+        return int(self.masses[x])
+
+    def cdf(self, x, i):
+        return int(self.cummasses[x]) + i
+
+    def icdf(self, cf):
+        x = int(np.searchsorted(self.cummasses, cf, side="right")) - 1
+        return x, cf - int(self.cummasses[x])
+
+    def push(self, m, x):
+        _check(lib().ans_cat_push(m.h, self.table, int(x)), "Categorical::push")
+
+    def pop(self, m):
+        x = u64(0)
+        _check(lib().ans_cat_pop(m.h, self.table, ctypes.byref(x)), "Categorical::pop")
+        return x.value
+
+    def prob(self, x):
+        return int(self.masses[x]) / self._norm
+
+    def entropy(self):
+        p = self.masses.astype(np.float64) / self._norm
+        p = p[p > 0]
+        return float(-(p * np.log2(p)).sum())
+
+
+class Bernoulli(Distribution):  # src/codec.rs:94-129
+    def __init__(self, mass, norm):
+        assert mass <= norm
+        self.categorical = Categorical([norm - mass, mass])
+
+    def norm(self):
+        return self.categorical.norm()
+
+    def pmf(self, x):
+        return self.categorical.pmf(int(bool(x)))
+
+    def cdf(self, x, i):
+        return self.categorical.cdf(int(bool(x)), i)
+
+    def icdf(self, cf):
+        x, i = self.categorical.icdf(cf)
+        return x != 0, i
+
+    def push(self, m, x):
+        self.categorical.push(m, int(bool(x)))
+
+    def pop(self, m):
+        return self.categorical.pop(m) != 0
+
+    def prob(self):
+        return self.categorical.prob(1)
+
+
+class IID(Codec):  # src/codec.rs:405-443
+    def __init__(self, item, length):
+        self.item = item
+        self.len = length
+
+    def push(self, m, x):
+        assert len(x) == self.len
+        if isinstance(self.item, Categorical):
+            s = np.ascontiguousarray(np.asarray(x, dtype=np.uint32))
+            _check(lib().ans_push_iid(m.h, self.item.table, _np_ptr(s), len(s)), "IID::push")
+            return
+        for e in reversed(list(x)):
+            self.item.push(m, e)
+
+    def pop(self, m):
+        if isinstance(self.item, Categorical):
+            out = np.zeros(max(self.len, 1), np.uint32)
+            _check(lib().ans_pop_iid(m.h, self.item.table, _np_ptr(out), self.len), "IID::pop")
+            return [int(v) for v in out[:self.len]]
+        return [self.item.pop(m) for _ in range(self.len)]
+
+    def bits(self, x):
+        total = 0.0
+        for e in x:
+            b = self.item.bits(e)
+            if b is None:
+                return None
+            total += b
+        return total
+
+
+class Independent(Codec):  # src/codec.rs:366-403
+    def __init__(self, codecs):
+        self.codecs = list(codecs)
+
+    def push(self, m, x):
+        assert len(x) == len(self.codecs)
+        for c, e in reversed(list(zip(self.codecs, x))):
+            c.push(m, e)
+
+    def pop(self, m):
+        return [c.pop(m) for c in self.codecs]
+
+    def bits(self, x):
+        total = 0.0
+        for c, e in zip(self.codecs, x):
+            b = c.bits(e)
+            if b is None:
+                return None
+            total += b
+        return total
+
+
+# ============================================================== GPU bulk path (section 4)
+def device_count():
+    c = ci(0)
+    _check(lib().ans_gpu_device_count(ctypes.byref(c)))
+    return c.value
+
+
+class Gpu:
+    """One device context (owns a HIP stream)."""
+
+    def __init__(self, device=0):
+        h = vp()
+        _check(lib().ans_gpu_create(device, ctypes.byref(h)), f"ans_gpu_create({device})")
+        self.h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            _lib.ans_gpu_free(h)
+            self.h = None
+
+    def status(self, d_status, stream=None):
+        st = ci(0)
+        _check(lib().ans_dev_status(self.h, _dptr(d_status), _sptr(stream), ctypes.byref(st)), "ans_dev_status")
+        return st.value
+
+    def compact(self, d_slots, slot_cap, d_lens, d_offsets, nchunks, d_out, stream=None):
+        _check(lib().ans_dev_compact(self.h, _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_offsets), nchunks,
+                                     _dptr(d_out), _sptr(stream)), "ans_dev_compact")
+
+
+def _dptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def _sptr(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+_WIDTH = {np.dtype(np.uint8): 1, np.dtype(np.uint16): 2, np.dtype(np.uint32): 4}
+
+
+class GpuTable:
+    """A Categorical table uploaded to one device (ans_gpu_table)."""
+
+    def __init__(self, gpu, categorical):
+        self.gpu = gpu
+        self.categorical = categorical
+        h = vp()
+        _check(lib().ans_gpu_table_create(gpu.h, categorical.table, ctypes.byref(h)), "ans_gpu_table_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            _lib.ans_gpu_table_free(h)
+            self.h = None
+
+    def slot_capacity(self, chunk_len):
+        c = u64(0)
+        _check(lib().ans_gpu_slot_capacity(self.h, chunk_len, ctypes.byref(c)))
+        return c.value
+
+    # ---- host buffers
+    def encode_chunks(self, syms, chunk_len):
+        """syms: np array of uint8/16/32.  Returns (dense bytes, offsets u64, lens u64)."""
+        syms = np.ascontiguousarray(syms)
+        w = _WIDTH[syms.dtype]
+        n = len(syms)
+        nchunks = -(-n // chunk_len)
+        total = u64(0)
+        _check(lib().ans_gpu_encode_chunks(self.h, _np_ptr(syms), w, n, chunk_len, None, 0, None, None,
+                                           ctypes.byref(total)), "ans_gpu_encode_chunks(size)")
+        out = np.zeros(max(total.value, 1), np.uint8)
+        offsets = np.zeros(max(nchunks, 1), np.uint64)
+        lens = np.zeros(max(nchunks, 1), np.uint64)
+        _check(lib().ans_gpu_encode_chunks(self.h, _np_ptr(syms), w, n, chunk_len, _np_ptr(out), len(out),
+                                           _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
+               "ans_gpu_encode_chunks")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode_chunks(self, data, offsets, lens, n, chunk_len, dtype=np.uint32, gen_kind=GEN_ZEROS):
+        data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+        offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_decode_chunks(self.h, _np_ptr(data) if data.size else None, data.size,
+                                           _np_ptr(offsets), _np_ptr(lens), n, chunk_len, gen_kind, _np_ptr(out),
+                                           _WIDTH[np.dtype(dtype)]), "ans_gpu_decode_chunks")
+        return out[:n]
+
+    # ---- device buffers (torch tensors or raw pointers)
+    def dev_encode(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None):
+        _check(lib().ans_dev_encode_chunks(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, _dptr(d_slots), slot_cap,
+                                           _dptr(d_lens), _dptr(d_status), _sptr(stream)), "ans_dev_encode_chunks")
+
+    def dev_decode(self, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status,
+                   stream=None, gen_kind=GEN_ZEROS):
+        _check(lib().ans_dev_decode_chunks(self.h, _dptr(d_in), _dptr(d_offsets), slot_cap, _dptr(d_lens), n,
+                                           chunk_len, gen_kind, _dptr(d_syms), sym_bytes, _dptr(d_status),
+                                           _sptr(stream)), "ans_dev_decode_chunks")
+
+    def dev_gen_iid(self, seed, start, n, d_syms, sym_bytes, stream=None):
+        _check(lib().ans_dev_gen_iid(self.h, seed, start, n, _dptr(d_syms), sym_bytes, _sptr(stream)),
+               "ans_dev_gen_iid")
+
+
+# ============================================================== synthetic tables
+def splitmix64_np(x):
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def c3_masses():
+    """256 masses 1 + (splitmix64(0x5EED ^ s) mod 2^20): norm 139,224,331."""
+    s = np.arange(256, dtype=np.uint64)
+    return (np.uint64(1) + (splitmix64_np(np.uint64(0x5EED) ^ s) & np.uint64((1 << 20) - 1))).astype(np.uint64)
+
+
+def c4_masses():
+    """65,536 masses 1 + (splitmix64(0xC4 ^ s) mod 2^12): norm 134,561,356."""
+    s = np.arange(65536, dtype=np.uint64)
+    return (np.uint64(1) + (splitmix64_np(np.uint64(0xC4) ^ s) & np.uint64((1 << 12) - 1))).astype(np.uint64)
+
+
+def read_multiset(path):
+    """The reference harness' reader (src/multiset.rs:161-166): ", "-separated integers."""
+    with open(path) as f:
+        return [int(s) for s in f.read().split(", ")]
+
+
+def multiset_masses(probs, norm=1 << 28):
+    """max(1, (p * norm) as usize) (src/multiset.rs:169-170)."""
+    return [max(1, int(p * float(norm))) for p in probs]

@@ -1,0 +1,46 @@
+// ans_table.hpp — host-side table objects shared by the C ABI (ans_capi.cpp) and the
+// GPU launchers (ans_kernels.hip).
+#pragma once
+
+#include <cstdint>
+
+#include "ans_core.hpp"
+
+// Opaque C-ABI handles (include/ans_capi.h).
+struct ans_msg {
+    shuffle_coding::Message m;
+};
+
+struct ans_table {
+    shuffle_coding::Categorical cat;  // Categorical::new(masses)  src/codec.rs:72-80
+};
+
+namespace shuffle_coding {
+
+// One symbol's row of the device table (16 B, so a 256-symbol alphabet is 4 KiB of LDS).
+// Entry nsym is a sentinel {0, norm, 0} so the icdf search never runs past the end.
+struct DevSym {
+    uint32_t mass;  // pmf(x)                            src/codec.rs:63
+    uint32_t cum;   // cummasses[x]                      src/codec.rs:64
+    double rcp;     // 1.0 / mass, for the quotient estimate in the fast path
+};
+
+// Everything a kernel needs, passed by value in the kernel arguments.
+struct DevTable {
+    const DevSym* sym;       // nsym + 1 rows
+    const uint16_t* bucket;  // nbucket entries: bucket[j] = icdf(j << shift).x
+    uint32_t nsym;
+    uint32_t norm;           // sum of masses, < 2^32
+    uint32_t shift;          // icdf bucket width = 2^shift
+    uint32_t nbucket;
+    uint64_t K;              // MAX_MIN_HEAD / norm      (src/ans.rs:100,109)
+    uint64_t L;              // norm * K: decode lower bound of the head interval
+    double rcp_norm;         // 1.0 / norm
+    uint32_t fast;           // 2^16 <= norm <= 2^31: f64 quotient estimate is exact after one fix-up
+    uint32_t pmin;           // smallest non-zero mass (sizes the worst-case slot)
+};
+
+constexpr uint32_t kBucketBits = 12;
+constexpr uint32_t kLdsTableLimit = 64 * 1024;  // table + buckets staged in LDS when they fit
+
+}  // namespace shuffle_coding

@@ -1,0 +1,182 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and golden vectors.
+
+Bit-exact is the bar: every chunk's stream must equal the reference message's flattened
+bytes (src/ans.rs:255-260) for the same input and chunk boundaries, and decode must be
+lossless and return each message to Message::zeros() (src/ans.rs:55-57).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import ans_amd as A
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    return A.Gpu(0)
+
+
+def _roundtrip_vs_oracle(gpu, masses, syms, chunk_len, dtype):
+    cat = A.Categorical(masses)
+    gt = A.GpuTable(gpu, cat)
+    s = np.asarray(syms).astype(dtype)
+    data, offsets, lens = gt.encode_chunks(s, chunk_len)
+    odata, ooffsets, olens = orc.encode_chunks(masses, np.asarray(syms, np.uint32), chunk_len)
+    assert np.array_equal(lens, olens)
+    assert np.array_equal(offsets, ooffsets)
+    assert data.tobytes() == odata.tobytes()
+    back = gt.decode_chunks(data, offsets, lens, len(s), chunk_len, dtype)
+    assert np.array_equal(back, s)
+    return data, lens
+
+
+# ---------------------------------------------------------------- C1 / C2 (multiset fixtures)
+@pytest.mark.parametrize("size", [1000, 10000, 100000])
+@pytest.mark.parametrize("layout", ["single_chunk", "chunks64"])
+def test_multiset_fixtures_bit_exact(gpu, size, layout, multiset_masses, multiset_vectors, golden_multiset):
+    rec = golden_multiset["vectors"][str(size)][layout]
+    syms = multiset_vectors[size]
+    for dtype in (np.uint16, np.uint32):
+        data, lens = _roundtrip_vs_oracle(gpu, multiset_masses, syms, rec["chunk_len"], dtype)
+        assert [int(x) for x in lens] == rec["lens"]
+        assert hashlib.sha256(data.tobytes()).hexdigest() == rec["sha256"]
+        if "hex" in rec:
+            assert data.tobytes().hex() == rec["hex"]
+
+
+def test_golden_small_cases(gpu, golden_small):
+    for case in golden_small:
+        for dtype in (np.uint8, np.uint16, np.uint32):
+            if dtype == np.uint8 and len(case["masses"]) > 256:
+                continue
+            data, lens = _roundtrip_vs_oracle(gpu, case["masses"], case["syms"], case["chunk_len"], dtype)
+            assert data.tobytes().hex() == case["hex"], case["name"]
+
+
+# ---------------------------------------------------------------- randomized tables
+def _random_case(rng, nsym, lo, hi, zero_frac, n):
+    masses = rng.integers(lo, hi, size=nsym, dtype=np.int64).astype(np.uint64)
+    if zero_frac:
+        masses[rng.random(nsym) < zero_frac] = 0
+        masses[rng.integers(0, nsym)] = max(1, int(masses.max()))
+    nz = np.flatnonzero(masses)
+    p = masses[nz].astype(np.float64)
+    syms = rng.choice(nz, size=n, p=p / p.sum()).astype(np.uint32)
+    return masses, syms
+
+
+@pytest.mark.parametrize("nsym,lo,hi,zero_frac,chunk_len,n", [
+    (2, 1, 10, 0.0, 7, 1000),                   # Bernoulli-sized, tiny norm: generic path
+    (8, 0, 4, 0.3, 5, 777),                     # zero masses, norm < 2^16
+    (256, 1, 1 << 20, 0.0, 4096, 300_000),      # C3-like, fast path, LDS table
+    (256, 1, 1 << 20, 0.1, 1563, 100_000),      # zero masses inside the fast path
+    (1024, 1 << 10, 1 << 21, 0.0, 1, 3000),     # one symbol per chunk
+    (4096, 1, 1 << 12, 0.0, 999, 200_000),      # LDS-sized large alphabet
+    (65536, 1, 1 << 12, 0.0, 4096, 400_000),    # C4 alphabet: table from global memory
+    (300, 1 << 22, 1 << 24, 0.0, 512, 50_000),  # norm > 2^31: generic path
+    (3, 1, 2, 0.0, 100, 1000),                  # norm 3..6
+])
+def test_random_tables_bit_exact(gpu, nsym, lo, hi, zero_frac, chunk_len, n):
+    rng = np.random.default_rng(nsym * 7919 + n)
+    masses, syms = _random_case(rng, nsym, lo, hi, zero_frac, n)
+    dtypes = [np.uint32, np.uint16] + ([np.uint8] if nsym <= 256 else [])
+    for dtype in dtypes:
+        _roundtrip_vs_oracle(gpu, masses, syms, chunk_len, dtype)
+
+
+def test_ragged_and_empty_inputs(gpu):
+    masses = [5, 9, 1, 300000, 17]
+    rng = np.random.default_rng(5)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    for n, chunk_len in [(0, 4), (1, 4), (3, 4), (4, 4), (5, 4), (4097, 4096), (10, 1000)]:
+        syms = rng.integers(0, 5, size=n).astype(np.uint32)
+        data, offsets, lens = gt.encode_chunks(syms, chunk_len)
+        od, oo, ol = orc.encode_chunks(masses, syms, chunk_len)
+        assert data.tobytes() == od.tobytes() and np.array_equal(lens, ol)
+        assert np.array_equal(gt.decode_chunks(data, offsets, lens, n, chunk_len), syms)
+
+
+def test_device_errors_mirror_reference_panics(gpu):
+    gt = A.GpuTable(gpu, A.Categorical([3, 0, 2]))
+    with pytest.raises(A.AnsError) as e:
+        gt.encode_chunks(np.array([0, 1, 2], np.uint32), 2)  # src/ans.rs:98
+    assert e.value.code == A.ANS_E_ZERO_MASS
+    with pytest.raises(A.AnsError) as e:
+        gt.encode_chunks(np.array([0, 3, 2], np.uint32), 2)  # src/codec.rs:63
+    assert e.value.code == A.ANS_E_SYMBOL
+    syms = np.array([0, 2, 2, 0, 2, 0, 0, 2], np.uint32)
+    data, offsets, lens = gt.encode_chunks(syms, 8)
+    # a truncated stream under Message::empty() exhausts the tail (src/ans.rs:144)
+    with pytest.raises(A.AnsError) as e:
+        gt.decode_chunks(data[1:], offsets, lens - 1, 8, 8, gen_kind=A.GEN_EMPTY)
+    assert e.value.code == A.ANS_E_EXHAUSTED
+    # ... and under Message::zeros() it does not return to the initial message (src/ans.rs:56)
+    with pytest.raises(A.AnsError) as e:
+        gt.decode_chunks(data[1:], offsets, lens - 1, 8, 8)
+    assert e.value.code == A.ANS_E_MISMATCH
+    with pytest.raises(A.AnsError) as e:
+        A.GpuTable(gpu, A.Categorical([1 << 31, 1 << 31]))  # norm >= 2^32 unsupported on the GPU
+    assert e.value.code == A.ANS_E_NORM_RANGE
+
+
+# ---------------------------------------------------------------- synthetic generator
+def test_gen_iid_matches_oracle(gpu):
+    torch = pytest.importorskip("torch")
+    masses = A.c3_masses()
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    n, start = 1 << 20, 12345
+    d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gt.dev_gen_iid(1, start, n, d, 1, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), orc.gen_iid(masses, 1, start, n).astype(np.uint8))
+
+
+# ---------------------------------------------------------------- full-size configs (device-resident)
+def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed, sample_chunks):
+    torch = pytest.importorskip("torch")
+    dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    stream = torch.cuda.current_stream()
+    nchunks = -(-n // chunk_len)
+    cap = gt.slot_capacity(chunk_len)
+    syms = torch.empty(n, dtype=dt, device="cuda")
+    gt.dev_gen_iid(seed, 0, n, syms, sym_bytes, stream)
+    slots = torch.empty(nchunks * cap, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    gt.dev_encode(syms, sym_bytes, n, chunk_len, slots, cap, lens, status, stream)
+    out = torch.empty_like(syms)
+    gt.dev_decode(slots, None, cap, lens, n, chunk_len, out, sym_bytes, status, stream)
+    assert gpu.status(status, stream) == 0
+    assert torch.equal(out, syms), "lossless round trip"
+    # bit-exact on a sample of chunks against the oracle
+    rng = np.random.default_rng(seed)
+    picks = sorted(set(rng.integers(0, nchunks, size=sample_chunks).tolist()) | {0, nchunks - 1})
+    lens_h = lens.cpu().numpy().astype(np.int64)
+    for j in picks:
+        a, b = j * chunk_len, min(n, (j + 1) * chunk_len)
+        ref_syms = orc.gen_iid(masses, seed, a, b - a)
+        got_syms = syms[a:b].cpu().numpy().astype(np.int64) & ((1 << (8 * sym_bytes)) - 1)
+        assert np.array_equal(got_syms, ref_syms)
+        od, _, ol = orc.encode_chunks(masses, ref_syms, chunk_len)
+        assert int(ol[0]) == lens_h[j]
+        got = slots[j * cap: j * cap + int(lens_h[j])].cpu().numpy()
+        assert got.tobytes() == od.tobytes(), f"chunk {j}"
+    return int(lens_h.sum())
+
+
+def test_c3_one_gib_u8_round_trip(gpu):
+    # 2^30 u8 symbols, 256-symbol table (norm 139,224,331), chunk 4096
+    total = _device_roundtrip(gpu, A.c3_masses(), 1 << 30, 4096, 1, 1, 48)
+    bps = total / (1 << 30)
+    assert 0.95 < bps < 0.99  # H = 7.738 bits -> ~0.967 B/symbol plus per-chunk flush
+
+
+def test_c4_shard_u16_round_trip(gpu):
+    # SURVEY.md §8d C4 table (65,536 symbols, norm 134,561,356); one 2^27-symbol shard
+    total = _device_roundtrip(gpu, A.c4_masses(), 1 << 27, 4096, 2, 2, 32)
+    assert 1.9 < total / (1 << 27) < 2.1
