@@ -125,7 +125,10 @@ def main():
     gpu = A.Gpu(local)
     gt = A.GpuTable(gpu, A.Categorical(masses))
     cap = gt.slot_capacity(L)
-    stream = torch.cuda.current_stream()
+    # all work on one explicit stream (torch's default stream handle is NULL, which the C ABI
+    # reads as "the context's own stream"); HIP events are recorded on this same stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
     syms = torch.empty(n, dtype=dt, device="cuda")
     gt.dev_gen_iid(seed, rank * n, n, syms, sym_bytes, stream)  # this rank's slice of the global array

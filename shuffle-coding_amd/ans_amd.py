@@ -95,6 +95,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run `make -C shuffle-coding_amd` (or __graft_entry__.build())")
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same soname).
+        # Loading torch first makes the dynamic loader bind our library to that copy, so
+        # device pointers and streams from torch are valid in our kernels.  Without torch
+        # the library binds to /opt/rocm's runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

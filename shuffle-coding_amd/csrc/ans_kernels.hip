@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <vector>
 
+#include "ans_fast.hpp"
 #include "ans_table.hpp"
 
 using namespace shuffle_coding;
@@ -30,6 +31,8 @@ struct ans_gpu_table {
     DevTable t;
     void* d_mem;
     uint32_t lds_bytes;  // 0 = table read from global memory (L2-resident)
+    FastTable ft;        // throughput path (ans_fast.hpp) when ft.usable
+    void* d_fast;
 };
 
 namespace {
@@ -142,7 +145,8 @@ struct ByteSource {
 // Encode: lane = chunk; symbols consumed last -> first (IID::push, src/codec.rs:417).
 template <typename Sym, bool kLds, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __restrict__ syms, uint64_t n,
-                                                   uint64_t chunk_len, uint64_t nchunks, uint8_t* __restrict__ slots,
+                                                   uint64_t chunk_len, uint64_t c_first, uint64_t nchunks,
+                                                   uint8_t* __restrict__ slots,
                                                    uint64_t slot_cap, uint32_t* __restrict__ lens,
                                                    uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __rest
         stage_table<false>(t, lds);
         rows = reinterpret_cast<const DevSym*>(lds);
     }
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t c = c_first + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (c >= nchunks) return;
     const uint64_t a = c * chunk_len;
     const uint64_t b = min(a + chunk_len, n);
@@ -201,7 +205,7 @@ template <typename Sym, bool kLds, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ offsets, uint64_t slot_cap,
                                                    const uint32_t* __restrict__ lens, uint64_t n, uint64_t chunk_len,
-                                                   uint64_t nchunks, int gen_kind, Sym* __restrict__ out,
+                                                   uint64_t c_first, uint64_t nchunks, int gen_kind, Sym* __restrict__ out,
                                                    uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
     const DevSym* rows = t.sym;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
         rows = reinterpret_cast<const DevSym*>(lds);
         bucket = reinterpret_cast<const uint16_t*>(lds + sizeof(DevSym) * (t.nsym + 1));
     }
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t c = c_first + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (c >= nchunks) return;
     const uint64_t a = c * chunk_len;
     const uint64_t b = min(a + chunk_len, n);
@@ -307,6 +311,16 @@ inline hipStream_t pick(ans_gpu_table* gt, void* stream) {
 
 inline unsigned grid_for(uint64_t lanes) { return static_cast<unsigned>((lanes + kBlock - 1) / kBlock); }
 
+// Full chunks whose symbols tile into 16-byte units go to the fast kernel when the table
+// allows it; everything else (ragged last chunk, odd chunk lengths, other tables) to the
+// generic kernel.  Both write the same slot layout and identical bytes.
+template <typename Sym>
+uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len) {
+    if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % 16 != 0) return 0;
+    if (sizeof(Sym) == 1 && gt->ft.nsym > 256) return 0;
+    return n / chunk_len;
+}
+
 template <typename Sym>
 int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t chunk_len, uint8_t* d_slots,
                   uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s) {
@@ -314,16 +328,30 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     const Sym* syms = static_cast<const Sym*>(d_syms);
-    const unsigned grid = grid_for(nchunks);
+    const uint64_t nfull = fast_chunks<Sym>(gt, n, chunk_len);
+    if (nfull) {
+        const FastTable& ft = gt->ft;
+        const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
+        const size_t lds = ft.enc_lds_bytes + sizeof(uint32_t) * fast::kRingDwords * fast::kBlock;
+        switch (ft.kmax) {
+        case 1:
+        case 2: fast::k_encode<Sym, 2><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status); break;
+        case 3: fast::k_encode<Sym, 3><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status); break;
+        default: fast::k_encode<Sym, 4><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status); break;
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    if (nfull == nchunks) return ANS_OK;
+    const unsigned grid = grid_for(nchunks - nfull);
     const size_t lds = gt->lds_bytes ? sizeof(DevSym) * (t.nsym + 1) : 0;
     if (gt->lds_bytes && t.fast)
-        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     else if (gt->lds_bytes)
-        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     else if (t.fast)
-        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     else
-        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -336,16 +364,26 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     Sym* out = static_cast<Sym*>(d_syms);
-    const unsigned grid = grid_for(nchunks);
+    // the fast kernel reads the encoder's 64-byte-aligned slot layout only
+    const uint64_t nfull = (d_offsets == nullptr && slot_cap % 64 == 0) ? fast_chunks<Sym>(gt, n, chunk_len) : 0;
+    if (nfull) {
+        const FastTable& ft = gt->ft;
+        const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
+        const size_t lds = ft.dec_lds_bytes + sizeof(uint32_t) * fast::kRingDwords * fast::kBlock;
+        fast::k_decode<Sym><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+        HIP_TRY(hipGetLastError());
+    }
+    if (nfull == nchunks) return ANS_OK;
+    const unsigned grid = grid_for(nchunks - nfull);
     const size_t lds = gt->lds_bytes;
     if (gt->lds_bytes && t.fast)
-        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
     else if (gt->lds_bytes)
-        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
     else if (t.fast)
-        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
     else
-        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -377,6 +415,78 @@ struct DevBuf {
     ~DevBuf() { if (p) (void)hipFree(p); }
     hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
 };
+
+// Derives the fast-path tables (ans_table.hpp FastTable) when the table qualifies:
+// 2^16 <= norm <= 2^31 (f64 quotient estimate) and nsym <= 256 (LDS-resident
+// rows and 8-bit icdf buckets).
+int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
+    const DevTable& t = gt->t;
+    FastTable ft{};
+    if (!t.fast || t.nsym > 256) {
+        gt->ft = ft;
+        return ANS_OK;
+    }
+    using u128 = unsigned __int128;
+    const uint32_t nsym = t.nsym;
+    std::vector<EncRow> enc(nsym + 1);
+    uint32_t kmax = 1;
+    for (uint32_t s = 0; s <= nsym; ++s) {
+        EncRow r{};
+        const uint64_t m = s < nsym ? cat.masses[s] : 0;
+        r.mass = static_cast<uint32_t>(m);
+        r.cum = s < nsym ? static_cast<uint32_t>(cat.cummasses[s]) : t.norm;
+        r.rcp = m ? 1.0 / static_cast<double>(m) : 0.0;
+        const u128 pK = static_cast<u128>(m) * t.K;
+        uint32_t kb = 0;
+        for (int j = 0; j < 4; ++j) {
+            const u128 thr = pK << (8 * (j + 1));  // p*K*2^(8(j+1)) < 2^96: no u128 overflow
+            if (thr == 0 || thr > (static_cast<u128>(1) << 64)) r.u[j] = ~0ull;  // unreachable
+            else {
+                r.u[j] = static_cast<uint64_t>(thr - 1);
+                if (m && thr < (static_cast<u128>(1) << 64)) kb = j + 1;
+            }
+        }
+        if (m && kb > kmax) kmax = kb;
+        enc[s] = r;
+    }
+    std::vector<DecRow> dec(nsym);
+    for (uint32_t s = 0; s < nsym; ++s)
+        dec[s] = DecRow{static_cast<uint32_t>(cat.cummasses[s]), static_cast<uint32_t>(cat.masses[s]),
+                        static_cast<uint32_t>(cat.cummasses[s] + cat.masses[s]), 0};
+    uint32_t bits = 0;
+    while (bits < 32 && (1ull << bits) < t.norm) ++bits;
+    ft.shift8 = bits > 13 ? bits - 13 : 0;  // <= 8192 one-byte buckets
+    const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(t.norm) + (1ull << ft.shift8) - 1) >> ft.shift8);
+    ft.bucket_lds_bytes = (nb + 15) & ~15u;
+    std::vector<uint8_t> bucket(ft.bucket_lds_bytes, 0);
+    for (uint32_t j = 0; j < nb; ++j)
+        bucket[j] = static_cast<uint8_t>(cat.icdf(static_cast<uint64_t>(j) << ft.shift8).first);
+    ft.nsym = nsym;
+    ft.enc_rows = nsym + 1;
+    ft.norm = t.norm;
+    ft.enc_lds_bytes = static_cast<uint32_t>((sizeof(EncRow) * enc.size() + 15) & ~size_t(15));
+    ft.dec_lds_bytes = ft.bucket_lds_bytes + static_cast<uint32_t>((sizeof(DecRow) * dec.size() + 15) & ~size_t(15));
+    ft.kmax = kmax;
+    ft.K = t.K;
+    ft.L = t.L;
+    ft.rcp_norm = t.rcp_norm;
+    const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = sizeof(DecRow) * dec.size();
+    const size_t o_dec = (enc_b + 255) & ~size_t(255), o_bkt = o_dec + ((dec_b + 255) & ~size_t(255));
+    HIP_TRY(hipSetDevice(gt->g->device));
+    void* mem = nullptr;
+    HIP_TRY(hipMalloc(&mem, o_bkt + bucket.size()));
+    gt->d_fast = mem;
+    char* base = static_cast<char*>(mem);
+    HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_dec, dec.data(), dec_b, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_bkt, bucket.data(), bucket.size(), hipMemcpyHostToDevice));
+    ft.enc = reinterpret_cast<const EncRow*>(base);
+    ft.dec = reinterpret_cast<const DecRow*>(base + o_dec);
+    ft.bucket8 = reinterpret_cast<const uint8_t*>(base + o_bkt);
+    ft.usable = 1;
+    gt->ft = ft;
+    return ANS_OK;
+}
 
 }  // namespace
 
@@ -454,9 +564,14 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
     HIP_TRY(hipMemcpy(static_cast<char*>(mem) + rows_bytes, buckets.data(), bucket_bytes, hipMemcpyHostToDevice));
     t.sym = static_cast<const DevSym*>(mem);
     t.bucket = reinterpret_cast<const uint16_t*>(static_cast<char*>(mem) + rows_bytes);
-    auto* gt = new (std::nothrow) ans_gpu_table{g, t, mem, 0};
+    auto* gt = new (std::nothrow) ans_gpu_table{g, t, mem, 0, FastTable{}, nullptr};
     if (!gt) { (void)hipFree(mem); return ANS_E_ALLOC; }
     if (rows_bytes + bucket_bytes <= kLdsTableLimit) gt->lds_bytes = static_cast<uint32_t>(rows_bytes + bucket_bytes);
+    const int rc = build_fast_table(gt, cat);
+    if (rc) {
+        ans_gpu_table_free(gt);
+        return rc;
+    }
     *out = gt;
     return ANS_OK;
 }
@@ -465,6 +580,7 @@ void ans_gpu_table_free(ans_gpu_table* gt) {
     if (!gt) return;
     (void)hipSetDevice(gt->g->device);
     (void)hipFree(gt->d_mem);
+    if (gt->d_fast) (void)hipFree(gt->d_fast);
     delete gt;
 }
 
@@ -475,8 +591,9 @@ int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t*
     const double per_sym = std::log2(static_cast<double>(gt->t.norm) / static_cast<double>(gt->t.pmin)) +
                            2.0 / static_cast<double>(gt->t.K) + 1e-6;
     const double bytes = (static_cast<double>(chunk_len) * per_sym + 2.0) / 8.0 + 9.0;
-    uint64_t cap = static_cast<uint64_t>(std::ceil(bytes)) + 8;
-    *slot_cap = (cap + 15) & ~uint64_t(15);
+    // + one page of slack: the fast encoder writes whole 64-byte pages (ans_fast.hpp)
+    const uint64_t cap = static_cast<uint64_t>(std::ceil(bytes)) + 8 + 64;
+    *slot_cap = (cap + 127) & ~uint64_t(127);
     return ANS_OK;
 }
 

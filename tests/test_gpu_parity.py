@@ -79,6 +79,13 @@ def _random_case(rng, nsym, lo, hi, zero_frac, n):
     (65536, 1, 1 << 12, 0.0, 4096, 400_000),    # C4 alphabet: table from global memory
     (300, 1 << 22, 1 << 24, 0.0, 512, 50_000),  # norm > 2^31: generic path
     (3, 1, 2, 0.0, 100, 1000),                  # norm 3..6
+    # fast-kernel shapes (chunk_len * width a multiple of 16, >= 512 chunks, ragged tail)
+    (256, 1, 1 << 20, 0.0, 64, 100_003),
+    (256, 1, 1 << 20, 0.2, 256, 300_017),       # zero masses inside the fast path
+    (200, 1 << 8, 1 << 22, 0.0, 1024, 600_000),  # nsym < 256: clamp sentinel
+    (17, 1 << 14, 1 << 15, 0.0, 512, 400_000),  # very skewed bytes/symbol (kmax 2)
+    (256, 1, 1 << 8, 0.0, 128, 200_000),        # norm ~2^15: generic path for every chunk
+    (256, 1, 1 << 23, 0.0, 2048, 1_000_000),    # norm ~2^31: top of the fast range
 ])
 def test_random_tables_bit_exact(gpu, nsym, lo, hi, zero_frac, chunk_len, n):
     rng = np.random.default_rng(nsym * 7919 + n)
@@ -123,14 +130,36 @@ def test_device_errors_mirror_reference_panics(gpu):
     assert e.value.code == A.ANS_E_NORM_RANGE
 
 
+def test_fast_kernel_errors(gpu):
+    masses = A.c3_masses().copy()
+    masses[7] = 0
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    syms = np.asarray(orc.gen_iid(masses, 3, 0, 64 * 4096), np.uint8)
+    data, offsets, lens = gt.encode_chunks(syms, 4096)  # no symbol 7 was generated
+    bad = syms.copy()
+    bad[5 * 4096 + 17] = 7
+    with pytest.raises(A.AnsError) as e:
+        gt.encode_chunks(bad, 4096)
+    assert e.value.code == A.ANS_E_ZERO_MASS
+    gt2 = A.GpuTable(gpu, A.Categorical(masses[:200]))
+    s2 = np.minimum(syms, 150).astype(np.uint8)
+    s2[s2 == 7] = 8
+    s2[3 * 4096 + 5] = 230  # out of range for a 200-symbol table
+    with pytest.raises(A.AnsError) as e:
+        gt2.encode_chunks(s2, 4096)
+    assert e.value.code == A.ANS_E_SYMBOL
+
+
 # ---------------------------------------------------------------- synthetic generator
 def test_gen_iid_matches_oracle(gpu):
     torch = pytest.importorskip("torch")
     masses = A.c3_masses()
     gt = A.GpuTable(gpu, A.Categorical(masses))
     n, start = 1 << 20, 12345
-    d = torch.empty(n, dtype=torch.uint8, device="cuda")
-    gt.dev_gen_iid(1, start, n, d, 1, torch.cuda.current_stream())
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        d = torch.empty(n, dtype=torch.uint8, device="cuda")
+        gt.dev_gen_iid(1, start, n, d, 1, stream)
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy(), orc.gen_iid(masses, 1, start, n).astype(np.uint8))
 
@@ -140,7 +169,8 @@ def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed, sample_chunks)
     torch = pytest.importorskip("torch")
     dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
     gt = A.GpuTable(gpu, A.Categorical(masses))
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream: torch's default stream handle is NULL
+    torch.cuda.set_stream(stream)
     nchunks = -(-n // chunk_len)
     cap = gt.slot_capacity(chunk_len)
     syms = torch.empty(n, dtype=dt, device="cuda")
@@ -153,6 +183,8 @@ def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed, sample_chunks)
     gt.dev_decode(slots, None, cap, lens, n, chunk_len, out, sym_bytes, status, stream)
     assert gpu.status(status, stream) == 0
     assert torch.equal(out, syms), "lossless round trip"
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(torch.cuda.default_stream())
     # bit-exact on a sample of chunks against the oracle
     rng = np.random.default_rng(seed)
     picks = sorted(set(rng.integers(0, nchunks, size=sample_chunks).tolist()) | {0, nchunks - 1})

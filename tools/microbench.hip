@@ -1,0 +1,126 @@
+// tools/microbench.hip — issue-rate microbenchmark of the VALU instructions the rANS
+// inner loops are built from (64-bit integer multiply, FP64, 64-bit shifts/compares).
+// Build: hipcc --offload-arch=gfx950 -O3 tools/microbench.hip -o tools/microbench
+// Prints wave-instructions per cycle per CU for 8 independent chains per lane.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#define ITERS 2048
+
+#define KERNEL(NAME, DECL, INIT, BODY, SINK)                                       \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, unsigned seed) {     \
+        DECL;                                                                       \
+        INIT;                                                                       \
+        for (int it = 0; it < ITERS; ++it) {                                        \
+            BODY;                                                                   \
+        }                                                                           \
+        SINK;                                                                       \
+    }
+
+// 32-bit ops: 8 chains a0..a7
+#define DECL32 unsigned a0, a1, a2, a3, a4, a5, a6, a7
+#define INIT32                                                                         \
+    a0 = threadIdx.x ^ seed; a1 = a0 + 1; a2 = a0 + 2; a3 = a0 + 3; a4 = a0 + 4;       \
+    a5 = a0 + 5; a6 = a0 + 6; a7 = a0 + 7
+#define SINK32 out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7
+#define OP32(INS)                                                                        \
+    asm volatile(INS " %0, %0, %1" : "+v"(a0) : "v"(a1));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a1) : "v"(a2));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a2) : "v"(a3));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a3) : "v"(a4));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a4) : "v"(a5));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a5) : "v"(a6));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a6) : "v"(a7));                                \
+    asm volatile(INS " %0, %0, %1" : "+v"(a7) : "v"(a0))
+
+KERNEL(k_add_u32, DECL32, INIT32, OP32("v_add_u32"), SINK32)
+KERNEL(k_mul_lo_u32, DECL32, INIT32, OP32("v_mul_lo_u32"), SINK32)
+KERNEL(k_mul_hi_u32, DECL32, INIT32, OP32("v_mul_hi_u32"), SINK32)
+KERNEL(k_mul_u32_u24, DECL32, INIT32, OP32("v_mul_u32_u24"), SINK32)
+KERNEL(k_mul_hi_u32_u24, DECL32, INIT32, OP32("v_mul_hi_u32_u24"), SINK32)
+KERNEL(k_xor_b32, DECL32, INIT32, OP32("v_xor_b32"), SINK32)
+
+// 64-bit ops on pairs
+#define DECL64 unsigned long long b0, b1, b2, b3, b4, b5, b6, b7
+#define INIT64                                                                          \
+    b0 = (threadIdx.x ^ seed) * 0x9E3779B97F4A7C15ull; b1 = b0 + 1; b2 = b0 + 2;        \
+    b3 = b0 + 3; b4 = b0 + 4; b5 = b0 + 5; b6 = b0 + 6; b7 = b0 + 7
+#define SINK64 out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(b0 ^ b1 ^ b2 ^ b3 ^ b4 ^ b5 ^ b6 ^ b7)
+#define MAD64(D, S)                                                                       \
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(D) : "v"((unsigned)S), "v"((unsigned)(S >> 32)) : "vcc")
+#define OPMAD MAD64(b0, b1); MAD64(b1, b2); MAD64(b2, b3); MAD64(b3, b4); MAD64(b4, b5); MAD64(b5, b6); MAD64(b6, b7); MAD64(b7, b0)
+KERNEL(k_mad_u64_u32, DECL64, INIT64, OPMAD, SINK64)
+
+#define SH64(D, S) asm volatile("v_lshrrev_b64 %0, %1, %0" : "+v"(D) : "v"((unsigned)S))
+#define OPSH SH64(b0, b1); SH64(b1, b2); SH64(b2, b3); SH64(b3, b4); SH64(b4, b5); SH64(b5, b6); SH64(b6, b7); SH64(b7, b0)
+KERNEL(k_lshrrev_b64, DECL64, INIT64, OPSH, SINK64)
+
+#define LA64(D, S) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(D) : "v"(S))
+#define OPLA LA64(b0, b1); LA64(b1, b2); LA64(b2, b3); LA64(b3, b4); LA64(b4, b5); LA64(b5, b6); LA64(b6, b7); LA64(b7, b0)
+KERNEL(k_lshl_add_u64, DECL64, INIT64, OPLA, SINK64)
+
+#define DECLF double d0, d1, d2, d3, d4, d5, d6, d7
+#define INITF                                                                              \
+    d0 = (threadIdx.x ^ seed) * 1e-3; d1 = d0 + 1; d2 = d0 + 2; d3 = d0 + 3; d4 = d0 + 4; \
+    d5 = d0 + 5; d6 = d0 + 6; d7 = d0 + 7
+#define SINKF out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7)
+#define FMA64(D, S) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(D) : "v"(S))
+#define OPFMA FMA64(d0, d1); FMA64(d1, d2); FMA64(d2, d3); FMA64(d3, d4); FMA64(d4, d5); FMA64(d5, d6); FMA64(d6, d7); FMA64(d7, d0)
+KERNEL(k_fma_f64, DECLF, INITF, OPFMA, SINKF)
+
+#define CVT(D, S) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(D) : "v"((unsigned)__double_as_longlong(S)))
+#define OPCVT CVT(d0, d1); CVT(d1, d2); CVT(d2, d3); CVT(d3, d4); CVT(d4, d5); CVT(d5, d6); CVT(d6, d7); CVT(d7, d0)
+KERNEL(k_cvt_f64_u32, DECLF, INITF, OPCVT, SINKF)
+
+#define DECLS float f0, f1, f2, f3, f4, f5, f6, f7
+#define INITS                                                                              \
+    f0 = (threadIdx.x ^ seed) * 1e-3f; f1 = f0 + 1; f2 = f0 + 2; f3 = f0 + 3; f4 = f0 + 4; \
+    f5 = f0 + 5; f6 = f0 + 6; f7 = f0 + 7
+#define SINKS out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7)
+#define FMA32(D, S) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(D) : "v"(S))
+#define OPFMA32 FMA32(f0, f1); FMA32(f1, f2); FMA32(f2, f3); FMA32(f3, f4); FMA32(f4, f5); FMA32(f5, f6); FMA32(f6, f7); FMA32(f7, f0)
+KERNEL(k_fma_f32, DECLS, INITS, OPFMA32, SINKS)
+
+#define CMP64(D, S) asm volatile("v_cmp_ge_u64 vcc, %0, %1\n\tv_cndmask_b32 %2, %2, 0, vcc" : "+v"(D) : "v"(S), "v"(a0) : "vcc")
+KERNEL(k_cmp_u64_cnd, DECL64; unsigned a0 = threadIdx.x, INIT64,
+       CMP64(b0, b1); CMP64(b1, b2); CMP64(b2, b3); CMP64(b3, b4); CMP64(b4, b5); CMP64(b5, b6); CMP64(b6, b7); CMP64(b7, b0),
+       SINK64 + a0)
+
+int main() {
+    const int blocks = 256 * 8, threads = 256;
+    unsigned* out;
+    hipMalloc(&out, sizeof(unsigned) * blocks * threads);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipDeviceProp_t prop;
+    hipGetDeviceProperties(&prop, 0);
+    const double clk_hz = prop.clockRate * 1e3;  // kHz -> Hz (max clock)
+    struct K { const char* name; void (*fn)(unsigned*, unsigned); int instr_per_op; };
+    K ks[] = {
+        {"v_add_u32", k_add_u32, 1},        {"v_xor_b32", k_xor_b32, 1},
+        {"v_mul_lo_u32", k_mul_lo_u32, 1},  {"v_mul_hi_u32", k_mul_hi_u32, 1},
+        {"v_mul_u32_u24", k_mul_u32_u24, 1}, {"v_mul_hi_u32_u24", k_mul_hi_u32_u24, 1},
+        {"v_mad_u64_u32", k_mad_u64_u32, 1}, {"v_lshrrev_b64", k_lshrrev_b64, 1},
+        {"v_lshl_add_u64", k_lshl_add_u64, 1}, {"v_fma_f64", k_fma_f64, 1},
+        {"v_cvt_f64_u32", k_cvt_f64_u32, 1}, {"v_fma_f32", k_fma_f32, 1},
+        {"v_cmp_ge_u64+v_cndmask", k_cmp_u64_cnd, 2},
+    };
+    printf("clock(max) %.0f MHz, CUs %d\n", clk_hz / 1e6, prop.multiProcessorCount);
+    for (auto& k : ks) {
+        hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(threads), 0, 0, out, 1u);
+        hipDeviceSynchronize();
+        hipEventRecord(e0);
+        for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(threads), 0, 0, out, 1u);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        const double wave_instr = 5.0 * blocks * (threads / 64.0) * ITERS * 8 * k.instr_per_op;
+        const double per_cu_per_clk = wave_instr / (ms * 1e-3) / prop.multiProcessorCount / clk_hz;
+        printf("%-24s %8.3f ms  %6.3f wave-instr/clk/CU  (%.2f cycles per wave-instr per SIMD)\n", k.name, ms,
+               per_cu_per_clk, 4.0 / per_cu_per_clk);
+    }
+    return 0;
+}
