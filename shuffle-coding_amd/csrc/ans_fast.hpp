@@ -2,16 +2,18 @@
 //
 // One lane = one chunk = one reference Message (src/ans.rs:292 zeros, src/codec.rs:415-424 IID,
 // src/ans.rs:96-116 push/pop, src/ans.rs:255-264 flatten/unflatten).  The bytes are identical
-// to the generic kernels' and to the oracle's; what changes is how the work maps to gfx950:
+// to the generic kernels' and to the oracle's; what changes is how the work maps to gfx950
+// (DESIGN.md §3 has the measurements behind each choice):
 //
 //  * Global memory is touched only at wave-uniform "points", one per 16-byte unit of symbols.
-//    Each point starts with `s_waitcnt vmcnt(0)`, so it waits only for what the previous point
-//    issued one unit earlier.  Symbol units are prefetched a point ahead (3-register rotation,
-//    no moves) and compressed bytes move between HBM and LDS as whole 64-byte pages.
-//  * Each lane stages its stream in a 128-byte LDS ring (two pages) with ALIGNED dword accesses
-//    only (unaligned LDS writes are ~7x slower on gfx950: tools/lds_probe.hip).  The ring's
-//    dword index is XOR-swizzled with the lane id: lanes advance at nearly the same rate and
-//    would otherwise all hit one bank.
+//    Each point starts with `s_waitcnt vmcnt(0)`, so it waits only for what earlier points
+//    issued.  Every global transfer is 64 contiguous bytes per lane (symbols in groups of
+//    four units, compressed streams in 64-byte pages): gfx950 HBM writes at 64-byte
+//    granularity, and 16-byte per-lane stores cost 4x their bytes in HBM traffic.
+//  * Each lane stages its stream in a 128-byte LDS ring (two pages) with ALIGNED dword
+//    accesses only (unaligned LDS writes are ~7x slower: tools/lds_probe.hip).  The ring is
+//    laid out [dword][lane], so any lane-varying index is bank-conflict free and a page is
+//    16 accesses at immediate offsets from one address.
 //  * Bytes move between the 64-bit head and the stream through v_alignbyte funnels.
 //  * q = head / p uses an f64 estimate and one integer fix-up, exact for
 //    2^16 <= norm <= 2^31.
@@ -28,6 +30,7 @@ namespace fast {
 
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
+constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
@@ -51,11 +54,12 @@ __device__ __forceinline__ uint64_t qest(uint64_t x, double rcp) {
     return static_cast<uint64_t>(__double_as_longlong(t)) - 0x4330000000000000ull;
 }
 
-// Lane-private ring of 32 dwords; physical slot XOR-swizzled by the lane id.
+// Lane-private ring of 32 dwords in a [dword][lane] image.
 struct Ring {
-    uint32_t* base;
-    uint32_t sw;
-    __device__ __forceinline__ uint32_t& at(int32_t i) const { return base[(static_cast<uint32_t>(i) ^ sw) & 31u]; }
+    uint32_t* base;  // &image[0][lane]
+    __device__ __forceinline__ uint32_t& at(int32_t i) const {
+        return base[(static_cast<uint32_t>(i) & 31u) * kBlock];
+    }
 };
 
 template <typename Sym>
@@ -109,51 +113,60 @@ __device__ __forceinline__ void flush_page(const Ring& ring, uint32_t p, uint8_t
     for (int q = 0; q < 4; ++q) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
-template <typename Sym, int KMAX>
+// KMAX: most bytes one push can emit (table property); kK32: K < 2^32 (norm > 2^24).
+template <typename Sym, int KMAX, bool kK32>
 __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
                                                       uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       uint32_t* __restrict__ lens, uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
     EncRow* rows = reinterpret_cast<EncRow*>(lds);
     for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) rows[i] = t.enc[i];
-    const Ring ring{reinterpret_cast<uint32_t*>(lds + t.enc_lds_bytes) + threadIdx.x * kRingDwords,
-                    threadIdx.x & 31u};
+    const Ring ring{reinterpret_cast<uint32_t*>(lds + t.enc_lds_bytes) + threadIdx.x};
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
-    const int nunit = static_cast<int>(chunk_len / U);
+    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / kGroupBytes);
     uint8_t* dst = slots + c * slot_cap;
     const uint32_t npages_cap = static_cast<uint32_t>(slot_cap / 64);
     const uint64_t norm = t.norm;
+    const uint64_t K = t.K;
     const uint32_t sentinel = t.enc_rows - 1;  // zero-mass row: out-of-range symbols land here
 
     uint64_t head = kMaxMinHead;  // Message::zeros()
     Funnel f{0, 0, 0, 0};
-    uint32_t fp = 0, bad = 0, over = 0;
+    uint32_t fp = 0, over = 0;
+    uint32_t minmass = ~0u;  // 0 after a zero-mass / out-of-range symbol; accumulated by an
+                             // opaque v_min so the compiler cannot sink the test to the loop end
+                             // (it did, keeping every row alive and spilling)
 
-    auto point = [&](uint4& slot, int v) {
+    auto point = [&]() __attribute__((always_inline)) {
         wait_vm();
         if ((f.wd >> 4) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
             if (fp < npages_cap) flush_page(ring, fp, dst);
             else over = 1;
             ++fp;
         }
-        slot = src[v > 0 ? v : 0];
     };
-    auto process = [&](const uint4& unit) {
+    auto process = [&](const uint4& unit) __attribute__((always_inline)) {
+        // rows are read one symbol ahead; the scheduling barriers keep the compiler from
+        // hoisting all sixteen reads (and their registers) to the top of the unit
+        EncRow e_next = rows[min(sym_of<Sym>(unit, U - 1), sentinel)];
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
-            const uint32_t x = min(sym_of<Sym>(unit, j), sentinel);
-            const EncRow e = rows[x];
-            bad |= e.mass == 0 ? 1u : 0u;
-            // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : head >= p*K*2^(8j)} bytes out
-            uint32_t k = head > e.u[0] ? 1u : 0u;
-            if constexpr (KMAX >= 2) k += head > e.u[1] ? 1u : 0u;
-            if constexpr (KMAX >= 3) k += head > e.u[2] ? 1u : 0u;
-            if constexpr (KMAX >= 4) k += head > e.u[3] ? 1u : 0u;
+            __builtin_amdgcn_sched_barrier(0);
+            const EncRow e = e_next;
+            if (j > 0) e_next = rows[min(sym_of<Sym>(unit, j - 1), sentinel)];
+            asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
+            // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
+            const uint64_t pK = kK32 ? static_cast<uint64_t>(e.mass) * static_cast<uint32_t>(K)
+                                     : static_cast<uint64_t>(e.mass) * K;
+            uint32_t k = (head >> 8) >= pK ? 1u : 0u;
+            if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 1u : 0u;
+            if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 1u : 0u;
+            if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
             f.push<KMAX>(lo32(head), k, ring);
             head >>= 8 * k;
             // q = head / p, r = head % p (src/ans.rs:101-102)
@@ -167,18 +180,32 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
         }
     };
 
-    uint4 A = src[nunit - 1], B = src[nunit >= 2 ? nunit - 2 : 0], C;
-    int u = nunit - 1;
-    for (;;) {
-        point(C, u - 2);
-        process(A);
-        if (--u < 0) break;
-        point(A, u - 2);
-        process(B);
-        if (--u < 0) break;
-        point(B, u - 2);
-        process(C);
-        if (--u < 0) break;
+    // groups are walked last to first; group g-1's 64 bytes are requested while g is coded
+    uint4 n0, n1, n2, n3;
+    {
+        const uint4* gsrc = src + 4 * (ngroups - 1);
+        n0 = gsrc[0];
+        n1 = gsrc[1];
+        n2 = gsrc[2];
+        n3 = gsrc[3];
+    }
+    for (int g = ngroups - 1; g >= 0; --g) {
+        point();
+        const uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+        {
+            const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
+            n0 = gsrc[0];
+            n1 = gsrc[1];
+            n2 = gsrc[2];
+            n3 = gsrc[3];
+        }
+        process(c3);
+        point();
+        process(c2);
+        point();
+        process(c1);
+        point();
+        process(c0);
     }
     wait_vm();
 
@@ -193,7 +220,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
         if (fp < npages_cap) flush_page(ring, fp, dst);
         else over = 1;
     }
-    if (bad) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
+    if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
         uint32_t sym_err = 0;
         for (uint64_t k = 0; k < chunk_len; ++k)
             sym_err |= static_cast<uint32_t>(syms[c * chunk_len + k]) >= t.nsym ? 1u : 0u;
@@ -215,12 +242,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
         const uint4* gb = reinterpret_cast<const uint4*>(t.bucket8);
         for (uint32_t i = threadIdx.x; i < t.bucket_lds_bytes / 16; i += kBlock) b[i] = gb[i];
         DecRow* r = reinterpret_cast<DecRow*>(lds + t.bucket_lds_bytes);
-        for (uint32_t i = threadIdx.x; i < t.nsym; i += kBlock) r[i] = t.dec[i];
+        for (uint32_t i = threadIdx.x; i < t.dec_rows; i += kBlock) r[i] = t.dec[i];
     }
     const uint8_t* bucket = lds;
     const DecRow* rows = reinterpret_cast<const DecRow*>(lds + t.bucket_lds_bytes);
-    const Ring ring{reinterpret_cast<uint32_t*>(lds + t.dec_lds_bytes) + threadIdx.x * kRingDwords,
-                    threadIdx.x & 31u};
+    const Ring ring{reinterpret_cast<uint32_t*>(lds + t.dec_lds_bytes) + threadIdx.x};
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;
@@ -236,13 +262,14 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     const uint32_t shift = t.shift8;
 
     // ---- pages: page p = stream bytes [64p, 64p+64), kept in ring half p&1
-    auto put_page = [&](int32_t p, const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3) {
+    auto put_page = [&](int32_t p, const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3)
+                        __attribute__((always_inline)) {
         const uint32_t w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
                                 v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
 #pragma unroll
         for (int i = 0; i < 16; ++i) ring.at(16 * p + i) = w[i];
     };
-    auto load_page_now = [&](int32_t p) {
+    auto load_page_now = [&](int32_t p) __attribute__((always_inline)) {
         const uint4* s = reinterpret_cast<const uint4*>(src + 64ll * p);
         put_page(p, s[0], s[1], s[2], s[3]);
     };
@@ -250,7 +277,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     if (len > 0) load_page_now(low);
     uint4 S0, S1, S2, S3;  // a page in flight between two points
     int32_t pend = -1;
-    auto request = [&](int32_t p) {
+    auto request = [&](int32_t p) __attribute__((always_inline)) {
         const uint4* s = reinterpret_cast<const uint4*>(src + 64ll * p);
         S0 = s[0];
         S1 = s[1];
@@ -258,7 +285,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
         S3 = s[3];
         pend = p;
     };
-    auto land = [&]() {
+    auto land = [&]() __attribute__((always_inline)) {
         put_page(pend, S0, S1, S2, S3);
         low = pend;
         pend = -1;
@@ -277,7 +304,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
         nd_idx = td - 1;
     }
     uint32_t nd = 0;
-    auto fetch_nd = [&]() {  // read dword nd_idx; serve lanes whose page has not landed yet
+    auto fetch_nd = [&]() __attribute__((always_inline)) {  // serve lanes whose page has not landed
         const bool starving = nd_idx >= 0 && (nd_idx >> 4) < low;
         if (__builtin_expect(__any(starving), 0)) {
             wait_vm();
@@ -290,17 +317,16 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
         nd = nd_idx >= 0 ? ring.at(nd_idx) : 0u;  // below the stream: TailGenerator bytes (0)
     };
     fetch_nd();
-    auto refill = [&]() {  // move nd into the window when nW <= 4
-        if (nW <= 4) {
-            const uint64_t wv = mk64(w1, w0) | ((static_cast<uint64_t>(nd) << 32) >> (8 * nW));
-            w1 = hi32(wv);
-            w0 = lo32(wv);
-            nW += 4;
-            nd_idx -= 1;
-        }
+    auto refill = [&]() __attribute__((always_inline)) {  // move nd into the window when nW <= 4
+        const bool take = nW <= 4;
+        const uint64_t wv = mk64(w1, w0) | ((static_cast<uint64_t>(nd) << 32) >> (8 * (nW & 7)));
+        w1 = take ? hi32(wv) : w1;
+        w0 = take ? lo32(wv) : w0;
+        nW += take ? 4u : 0u;
+        nd_idx -= take ? 1 : 0;
         fetch_nd();
     };
-    auto pull1 = [&](uint64_t h) -> uint64_t {
+    auto pull1 = [&](uint64_t h) __attribute__((always_inline)) -> uint64_t {
         if (nW == 0) refill();
         const uint32_t b = w1 >> 24;
         w1 = ab(w1, w0, 3);
@@ -313,10 +339,16 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     uint64_t head = 0;
     for (int g = 0; g < 9 && head < L; ++g) head = pull1(head);
 
-    uint4 outv = make_uint4(0, 0, 0, 0);
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0, outv = q0;
     for (int u = 0; u < nunit; ++u) {
         wait_vm();  // point: retire what the previous point issued
-        if (u > 0) dst[u - 1] = outv;
+        if (u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
+            uint4* d = dst + (u - 4);
+            d[0] = q0;
+            d[1] = q1;
+            d[2] = q2;
+            d[3] = q3;
+        }
         if (pend >= 0) land();
         if (pend < 0 && low > 0 && (nd_idx >> 4) <= low) request(low - 1);
 #pragma unroll
@@ -329,18 +361,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
             const uint32_t js = (64u - bl) >> 3;
             const uint32_t m = js - 1;
             const uint32_t s = (4u - m) & 3u;
-            uint32_t c1 = ab(h1, h0, s), c0 = ab(h0, w1, s);
-            c1 = m == 0 ? h1 : c1;
-            c0 = m == 0 ? h0 : c0;
-            const uint32_t k = js - ((js >= 1 && mk64(c1, c0) >= L) ? 1u : 0u);
+            const uint32_t c1 = m == 0 ? h1 : ab(h1, h0, s);
+            const uint32_t c0 = m == 0 ? h0 : ab(h0, w1, s);
+            const uint32_t k = js - ((js >= 1 ? 1u : 0u) & (mk64(c1, c0) >= L ? 1u : 0u));
             const uint32_t sk = (4u - k) & 3u;
-            const uint32_t n1 = ab(h1, h0, sk), n0 = ab(h0, w1, sk);
+            const bool nz = k != 0;
+            head = nz ? mk64(ab(h1, h0, sk), ab(h0, w1, sk)) : head;
             const uint32_t x1 = ab(w1, w0, sk), x0 = ab(w0, 0u, sk);
-            if (k != 0) {
-                head = mk64(n1, n0);
-                w1 = x1;
-                w0 = x0;
-            }
+            w1 = nz ? x1 : w1;
+            w0 = nz ? x0 : w0;
             nW -= k;
             // q = head / norm, cf = head % norm (src/ans.rs:110-111)
             uint64_t q = qest(head, rcp_norm);
@@ -348,16 +377,40 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
             const uint32_t neg = ii < 0 ? 1u : 0u;
             q -= neg;
             const uint32_t cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
-            // icdf (src/codec.rs:65-68): last symbol with cum <= cf
+            // icdf (src/codec.rs:65-68), last symbol with cum <= cf: the bucket gives s0, and
+            // rows s0..s0+2 settle it unless the table flags a narrow neighbourhood.
             uint32_t sx = bucket[cf >> shift];
-            DecRow e = rows[sx];
-            while (cf >= e.cum_next) e = rows[++sx];
-            head = q * e.mass + (cf - e.cum);  // src/ans.rs:113-114
+            const DecRow r0 = rows[sx], r1 = rows[sx + 1], r2 = rows[sx + 2];
+            const uint32_t b1 = cf >= r1.cum ? 1u : 0u, b2 = cf >= r2.cum ? 1u : 0u;
+            uint32_t cum = b2 ? r2.cum : (b1 ? r1.cum : r0.cum);
+            uint32_t mass = (b2 ? r2.mass : (b1 ? r1.mass : r0.mass)) & ~kDecMulti;
+            sx += b1 + b2;
+            const bool multi = (r0.mass & kDecMulti) != 0;
+            if (__builtin_expect(__any(multi), 0)) {
+                if (multi) {
+                    while (cf >= rows[sx + 1].cum) ++sx;
+                    cum = rows[sx].cum;
+                    mass = rows[sx].mass & ~kDecMulti;
+                }
+            }
+            head = q * mass + (cf - cum);  // src/ans.rs:113-114
             put_sym<Sym>(outv, j, sx);
+        }
+        switch (u & 3) {
+        case 0: q0 = outv; break;
+        case 1: q1 = outv; break;
+        case 2: q2 = outv; break;
+        default: q3 = outv; break;
         }
     }
     wait_vm();
-    if (nunit > 0) dst[nunit - 1] = outv;
+    if (nunit >= 4) {
+        uint4* d = dst + (nunit - 4);
+        d[0] = q0;
+        d[1] = q1;
+        d[2] = q2;
+        d[3] = q3;
+    }
 
     // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
     for (int g = 0; g < 9 && head < kMaxMinHead; ++g) head = pull1(head);

@@ -316,7 +316,7 @@ inline unsigned grid_for(uint64_t lanes) { return static_cast<unsigned>((lanes +
 // generic kernel.  Both write the same slot layout and identical bytes.
 template <typename Sym>
 uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len) {
-    if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % 16 != 0) return 0;
+    if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % fast::kGroupBytes != 0) return 0;
     if (sizeof(Sym) == 1 && gt->ft.nsym > 256) return 0;
     return n / chunk_len;
 }
@@ -333,12 +333,15 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         const size_t lds = ft.enc_lds_bytes + sizeof(uint32_t) * fast::kRingDwords * fast::kBlock;
+#define ENC(KM, K32) fast::k_encode<Sym, KM, K32><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
+        const bool k32 = ft.K < (1ull << 32);
         switch (ft.kmax) {
         case 1:
-        case 2: fast::k_encode<Sym, 2><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status); break;
-        case 3: fast::k_encode<Sym, 3><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status); break;
-        default: fast::k_encode<Sym, 4><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status); break;
+        case 2: if (k32) ENC(2, true); else ENC(2, false); break;
+        case 3: if (k32) ENC(3, true); else ENC(3, false); break;
+        default: if (k32) ENC(4, true); else ENC(4, false); break;
         }
+#undef ENC
         HIP_TRY(hipGetLastError());
     }
     if (nfull == nchunks) return ANS_OK;
@@ -431,38 +434,34 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     std::vector<EncRow> enc(nsym + 1);
     uint32_t kmax = 1;
     for (uint32_t s = 0; s <= nsym; ++s) {
-        EncRow r{};
         const uint64_t m = s < nsym ? cat.masses[s] : 0;
-        r.mass = static_cast<uint32_t>(m);
-        r.cum = s < nsym ? static_cast<uint32_t>(cat.cummasses[s]) : t.norm;
-        r.rcp = m ? 1.0 / static_cast<double>(m) : 0.0;
+        enc[s] = EncRow{m ? 1.0 / static_cast<double>(m) : 0.0, static_cast<uint32_t>(m),
+                        s < nsym ? static_cast<uint32_t>(cat.cummasses[s]) : t.norm};
+        if (!m) continue;
         const u128 pK = static_cast<u128>(m) * t.K;
-        uint32_t kb = 0;
-        for (int j = 0; j < 4; ++j) {
-            const u128 thr = pK << (8 * (j + 1));  // p*K*2^(8(j+1)) < 2^96: no u128 overflow
-            if (thr == 0 || thr > (static_cast<u128>(1) << 64)) r.u[j] = ~0ull;  // unreachable
-            else {
-                r.u[j] = static_cast<uint64_t>(thr - 1);
-                if (m && thr < (static_cast<u128>(1) << 64)) kb = j + 1;
-            }
-        }
-        if (m && kb > kmax) kmax = kb;
-        enc[s] = r;
+        for (uint32_t j = 1; j <= 4; ++j)  // can a push emit j bytes? (head < 2^64 <= p*K*2^8j otherwise)
+            if ((pK << (8 * j)) < (static_cast<u128>(1) << 64) && j > kmax) kmax = j;
     }
-    std::vector<DecRow> dec(nsym);
-    for (uint32_t s = 0; s < nsym; ++s)
-        dec[s] = DecRow{static_cast<uint32_t>(cat.cummasses[s]), static_cast<uint32_t>(cat.masses[s]),
-                        static_cast<uint32_t>(cat.cummasses[s] + cat.masses[s]), 0};
     uint32_t bits = 0;
     while (bits < 32 && (1ull << bits) < t.norm) ++bits;
     ft.shift8 = bits > 13 ? bits - 13 : 0;  // <= 8192 one-byte buckets
-    const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(t.norm) + (1ull << ft.shift8) - 1) >> ft.shift8);
+    const uint64_t width = 1ull << ft.shift8;
+    std::vector<DecRow> dec(nsym + 3, DecRow{t.norm, 0});
+    for (uint32_t s = 0; s < nsym; ++s) {
+        const uint64_t m1 = s + 1 < nsym ? cat.masses[s + 1] : width;
+        const uint64_t m2 = s + 2 < nsym ? cat.masses[s + 2] : width;
+        const bool multi = m1 + m2 < width;  // a bucket from s could reach past cum[s+3]
+        dec[s] = DecRow{static_cast<uint32_t>(cat.cummasses[s]),
+                        static_cast<uint32_t>(cat.masses[s]) | (multi ? kDecMulti : 0u)};
+    }
+    const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(t.norm) + width - 1) >> ft.shift8);
     ft.bucket_lds_bytes = (nb + 15) & ~15u;
     std::vector<uint8_t> bucket(ft.bucket_lds_bytes, 0);
     for (uint32_t j = 0; j < nb; ++j)
         bucket[j] = static_cast<uint8_t>(cat.icdf(static_cast<uint64_t>(j) << ft.shift8).first);
     ft.nsym = nsym;
     ft.enc_rows = nsym + 1;
+    ft.dec_rows = nsym + 3;
     ft.norm = t.norm;
     ft.enc_lds_bytes = static_cast<uint32_t>((sizeof(EncRow) * enc.size() + 15) & ~size_t(15));
     ft.dec_lds_bytes = ft.bucket_lds_bytes + static_cast<uint32_t>((sizeof(DecRow) * dec.size() + 15) & ~size_t(15));

@@ -44,33 +44,34 @@ constexpr uint32_t kBucketBits = 12;
 constexpr uint32_t kLdsTableLimit = 64 * 1024;  // table + buckets staged in LDS when they fit
 
 // ---- fast-path tables (ans_fast.hpp); built when FastTable::usable.
-// Encode row: u[j] = p*K*2^(8(j+1)) - 1 saturated at 2^64-1, so that the number of bytes
-// renorm_down emits (src/ans.rs:246-253) is #{j : head > u[j]} with no overflow corner.
+// Encode row (16 B, one ds_read_b128): the thresholds p*K*2^(8j) are formed in registers.
 struct EncRow {
-    uint64_t u[4];
-    double rcp;     // 1.0 / mass
+    double rcp;     // 1.0 / mass (0 for the zero-mass sentinel)
     uint32_t mass;
     uint32_t cum;
 };
-// Decode row: the symbol's cdf interval [cum, cum_next).
+// Decode row (8 B): symbol s covers cdf values [cum, cum + mass); row nsym is the sentinel
+// {norm, 0}.  Bit 31 of `mass` flags that a bucket starting in this symbol may contain
+// three or more cdf boundaries (rows s+1 and s+2 narrower than one bucket together).
 struct DecRow {
     uint32_t cum;
     uint32_t mass;
-    uint32_t cum_next;
-    uint32_t pad;
 };
+constexpr uint32_t kDecMulti = 0x80000000u;
 struct FastTable {
     const EncRow* enc;       // enc_rows = nsym + 1 rows (last = zero-mass sentinel)
-    const DecRow* dec;       // nsym rows
+    const DecRow* dec;       // nsym + 3 rows (sentinels) so s0 + 2 is always readable
     const uint8_t* bucket8;  // bucket8[j] = icdf(j << shift8).x, padded to bucket_lds_bytes
     uint32_t nsym;
     uint32_t enc_rows;
+    uint32_t dec_rows;
     uint32_t norm;
     uint32_t shift8;
     uint32_t enc_lds_bytes;     // LDS bytes of the staged encode rows (16-aligned)
     uint32_t bucket_lds_bytes;  // LDS bytes of the staged buckets (16-aligned)
     uint32_t dec_lds_bytes;     // buckets + decode rows (16-aligned)
     uint32_t kmax;              // max bytes one push emits (1..4)
+    uint32_t pad;
     uint64_t K;
     uint64_t L;
     double rcp_norm;
