@@ -31,6 +31,7 @@ namespace fast {
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
+constexpr uint32_t kDecTableBytes = 16384;  // decode buckets in LDS: 2 x (64 KiB ring + 16 KiB) per CU
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
@@ -231,115 +232,108 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
 }
 
 // ====================================================================== decode
+// The lane's stream pages land in its ring at points: page low+1 is consumed once the next
+// dword to read (nd_idx) lies below it, and the page below `low` is always in flight in
+// registers (S), so after a point the ring holds at least 16 unread dwords.  One unit pops
+// U symbols of at most KMAX <= 4 bytes each, <= 64 bytes = 16 dwords: no lane can run dry
+// between points, and the step needs no availability test.
 template <typename Sym>
-__global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots,
-                                                      uint64_t slot_cap, const uint32_t* __restrict__ lens,
-                                                      uint64_t chunk_len, uint64_t nfull, int gen_kind,
-                                                      Sym* __restrict__ out, uint32_t* __restrict__ status) {
+__global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                      const uint32_t* __restrict__ lens, uint64_t chunk_len,
+                                                      uint64_t nfull, int gen_kind, Sym* __restrict__ out,
+                                                      uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
     {
-        uint4* b = reinterpret_cast<uint4*>(lds);
-        const uint4* gb = reinterpret_cast<const uint4*>(t.bucket8);
-        for (uint32_t i = threadIdx.x; i < t.bucket_lds_bytes / 16; i += kBlock) b[i] = gb[i];
-        DecRow* r = reinterpret_cast<DecRow*>(lds + t.bucket_lds_bytes);
-        for (uint32_t i = threadIdx.x; i < t.dec_rows; i += kBlock) r[i] = t.dec[i];
+        uint2* b = reinterpret_cast<uint2*>(lds);
+        const uint2* gb = reinterpret_cast<const uint2*>(t.dbkt);
+        for (uint32_t i = threadIdx.x; i < 3 * t.dec_buckets; i += kBlock) b[i] = gb[i];
+        uint32_t* cl = reinterpret_cast<uint32_t*>(lds + t.dec_cum_off);
+        for (uint32_t i = threadIdx.x; i < t.nsym + 5; i += kBlock) cl[i] = t.cum[i];
     }
-    const uint8_t* bucket = lds;
-    const DecRow* rows = reinterpret_cast<const DecRow*>(lds + t.bucket_lds_bytes);
+    const unsigned char* bkt = lds;
+    const uint32_t* lcum = reinterpret_cast<const uint32_t*>(lds + t.dec_cum_off);
     const Ring ring{reinterpret_cast<uint32_t*>(lds + t.dec_lds_bytes) + threadIdx.x};
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
-    const uint8_t* src = slots + c * slot_cap;
-    const int32_t len = static_cast<int32_t>(lens[c]);
-    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
     const int nunit = static_cast<int>(chunk_len / U);
+    const uint8_t* src = slots + c * slot_cap;
+    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
+    const int32_t len = static_cast<int32_t>(lens[c]);
     const uint64_t L = t.L;
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
-    const uint32_t shift = t.shift8;
+    const uint32_t shift = t.dec_shift;
 
-    // ---- pages: page p = stream bytes [64p, 64p+64), kept in ring half p&1
-    auto put_page = [&](int32_t p, const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3)
-                        __attribute__((always_inline)) {
-        const uint32_t w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                                v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+    uint4 S[4];
+    auto put_page = [&](int32_t p) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) ring.at(16 * p + i) = w[i];
+        for (int k = 0; k < 4; ++k) {
+            ring.at(16 * p + 4 * k + 0) = S[k].x;
+            ring.at(16 * p + 4 * k + 1) = S[k].y;
+            ring.at(16 * p + 4 * k + 2) = S[k].z;
+            ring.at(16 * p + 4 * k + 3) = S[k].w;
+        }
     };
-    auto load_page_now = [&](int32_t p) __attribute__((always_inline)) {
-        const uint4* s = reinterpret_cast<const uint4*>(src + 64ll * p);
-        put_page(p, s[0], s[1], s[2], s[3]);
+    auto fetch_page = [&](int32_t p) __attribute__((always_inline)) {
+        const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) S[k] = g[k];
     };
-    int32_t low = len > 0 ? (len - 1) >> 6 : 0;  // lowest page present in the ring
-    if (len > 0) load_page_now(low);
-    uint4 S0, S1, S2, S3;  // a page in flight between two points
-    int32_t pend = -1;
-    auto request = [&](int32_t p) __attribute__((always_inline)) {
-        const uint4* s = reinterpret_cast<const uint4*>(src + 64ll * p);
-        S0 = s[0];
-        S1 = s[1];
-        S2 = s[2];
-        S3 = s[3];
-        pend = p;
-    };
-    auto land = [&]() __attribute__((always_inline)) {
-        put_page(pend, S0, S1, S2, S3);
-        low = pend;
-        pend = -1;
-    };
-    if (low >= 1) request(low - 1);
 
-    // ---- window: (w1:w0) holds nW stream bytes MSB-aligned (next byte to pop on top);
-    //      nd = stream dword nd_idx (the next one below the window), prefetched from the ring.
+    // the top two pages land before decoding starts; the third is requested
+    const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
+    int32_t low = top;
+    if (len > 0) {
+        fetch_page(top);
+        wait_vm();
+        put_page(top);
+    }
+    if (top >= 1) {
+        fetch_page(top - 1);
+        wait_vm();
+        put_page(top - 1);
+        low = top - 1;
+    }
+    bool pend = low >= 1;
+    if (pend) fetch_page(low - 1);
+
+    // window: (w1:w0) holds nW stream bytes MSB-aligned (next byte to pop on top);
+    // nd = stream dword nd_idx, the next one below the window (0 below the stream: the
+    // Zeros generator, src/ans.rs:160-170).
     uint32_t w1 = 0, w0 = 0, nW = 0;
     int32_t nd_idx = -1;
     if (len > 0) {
         const int32_t td = (len - 1) >> 2;
-        const uint32_t c0 = static_cast<uint32_t>(len - 4 * td);
-        w1 = ring.at(td) << (8 * (4 - c0));
-        nW = c0;
+        const uint32_t cb = static_cast<uint32_t>(len - 4 * td);
+        w1 = ring.at(td) << (8 * (4 - cb));
+        nW = cb;
         nd_idx = td - 1;
     }
-    uint32_t nd = 0;
-    auto fetch_nd = [&]() __attribute__((always_inline)) {  // serve lanes whose page has not landed
-        const bool starving = nd_idx >= 0 && (nd_idx >> 4) < low;
-        if (__builtin_expect(__any(starving), 0)) {
-            wait_vm();
-            if (starving && pend >= 0) land();
-            if (nd_idx >= 0 && (nd_idx >> 4) < low) {
-                load_page_now(nd_idx >> 4);
-                low = nd_idx >> 4;
-            }
-        }
-        nd = nd_idx >= 0 ? ring.at(nd_idx) : 0u;  // below the stream: TailGenerator bytes (0)
-    };
-    fetch_nd();
-    auto refill = [&]() __attribute__((always_inline)) {  // move nd into the window when nW <= 4
+    uint32_t nd = ring.at(nd_idx);
+    nd = nd_idx >= 0 ? nd : 0u;
+    auto refill = [&]() __attribute__((always_inline)) {  // nd into the window when nW <= 4
         const bool take = nW <= 4;
-        const uint64_t wv = mk64(w1, w0) | ((static_cast<uint64_t>(nd) << 32) >> (8 * (nW & 7)));
-        w1 = take ? hi32(wv) : w1;
-        w0 = take ? lo32(wv) : w0;
+        const uint64_t add = (static_cast<uint64_t>(nd) << 32) >> (8 * (nW & 7));
+        w1 = take ? (w1 | hi32(add)) : w1;
+        w0 = take ? lo32(add) : w0;
         nW += take ? 4u : 0u;
         nd_idx -= take ? 1 : 0;
-        fetch_nd();
+        const uint32_t v = ring.at(nd_idx);
+        nd = nd_idx >= 0 ? v : 0u;
     };
-    auto pull1 = [&](uint64_t h) __attribute__((always_inline)) -> uint64_t {
+    uint64_t head = 0;  // Message::unflatten: head 0, then renorm_up pulls the flushed head
+    for (int g = 0; g < 9 && head < L; ++g) {
         if (nW == 0) refill();
-        const uint32_t b = w1 >> 24;
+        head = (head << 8) | (w1 >> 24);
         w1 = ab(w1, w0, 3);
         w0 <<= 8;
         nW -= 1;
-        return (h << 8) | b;
-    };
+    }
 
-    // Message::unflatten (head = 0); the first renorm_up pulls the flushed head back in.
-    uint64_t head = 0;
-    for (int g = 0; g < 9 && head < L; ++g) head = pull1(head);
-
-    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0, outv = q0;
+    uint4 q0, q1, q2, q3;
     for (int u = 0; u < nunit; ++u) {
         wait_vm();  // point: retire what the previous point issued
         if (u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
@@ -349,21 +343,26 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
             d[2] = q2;
             d[3] = q3;
         }
-        if (pend >= 0) land();
-        if (pend < 0 && low > 0 && (nd_idx >> 4) <= low) request(low - 1);
+        if (pend && (nd_idx >> 4) <= low) {  // page low+1 consumed: land the page below
+            put_page(low - 1);
+            --low;
+            pend = low >= 1;
+            if (pend) fetch_page(low - 1);
+        }
+        uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             refill();
-            // renorm_up (src/ans.rs:239-243): k = min{j : top64((head:W) << 8j) >= L}.  With bl
-            // the head's bit length, js = (64 - bl) >> 3 bytes reach 2^56 >= L; js - 1 may too.
+            // renorm_up (src/ans.rs:239-243): k = min{j : top64((head:W) << 8j) >= L}.  With
+            // bl the head's bit length, js = (64 - bl) >> 3 bytes reach 2^56 >= L; js-1 may too.
             const uint32_t h1 = hi32(head), h0 = lo32(head);
             const uint32_t bl = 64u - static_cast<uint32_t>(__builtin_clzll(head | 1));
             const uint32_t js = (64u - bl) >> 3;
             const uint32_t m = js - 1;
-            const uint32_t s = (4u - m) & 3u;
-            const uint32_t c1 = m == 0 ? h1 : ab(h1, h0, s);
-            const uint32_t c0 = m == 0 ? h0 : ab(h0, w1, s);
-            const uint32_t k = js - ((js >= 1 ? 1u : 0u) & (mk64(c1, c0) >= L ? 1u : 0u));
+            const uint32_t sm = (4u - m) & 3u;
+            const uint32_t t1 = m == 0 ? h1 : ab(h1, h0, sm);
+            const uint32_t t0 = m == 0 ? h0 : ab(h0, w1, sm);
+            const uint32_t k = js - ((js >= 1 ? 1u : 0u) & (mk64(t1, t0) >= L ? 1u : 0u));
             const uint32_t sk = (4u - k) & 3u;
             const bool nz = k != 0;
             head = nz ? mk64(ab(h1, h0, sk), ab(h0, w1, sk)) : head;
@@ -372,28 +371,28 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
             w0 = nz ? x0 : w0;
             nW -= k;
             // q = head / norm, cf = head % norm (src/ans.rs:110-111)
-            uint64_t q = qest(head, rcp_norm);
-            const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
+            uint64_t qq = qest(head, rcp_norm);
+            const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(qq) * norm);
             const uint32_t neg = ii < 0 ? 1u : 0u;
-            q -= neg;
+            qq -= neg;
             const uint32_t cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
-            // icdf (src/codec.rs:65-68), last symbol with cum <= cf: the bucket gives s0, and
-            // rows s0..s0+2 settle it unless the table flags a narrow neighbourhood.
-            uint32_t sx = bucket[cf >> shift];
-            const DecRow r0 = rows[sx], r1 = rows[sx + 1], r2 = rows[sx + 2];
-            const uint32_t b1 = cf >= r1.cum ? 1u : 0u, b2 = cf >= r2.cum ? 1u : 0u;
-            uint32_t cum = b2 ? r2.cum : (b1 ? r1.cum : r0.cum);
-            uint32_t mass = (b2 ? r2.mass : (b1 ? r1.mass : r0.mass)) & ~kDecMulti;
-            sx += b1 + b2;
-            const bool multi = (r0.mass & kDecMulti) != 0;
-            if (__builtin_expect(__any(multi), 0)) {
-                if (multi) {
-                    while (cf >= rows[sx + 1].cum) ++sx;
-                    cum = rows[sx].cum;
-                    mass = rows[sx].mass & ~kDecMulti;
+            // icdf (src/codec.rs:65-68): the last symbol with cdf <= cf, from cf's bucket
+            const uint2* e = reinterpret_cast<const uint2*>(bkt + __umul24(cf >> shift, sizeof(DecBucket)));
+            const uint2 e01 = e[0], e23 = e[1], e4s = e[2];
+            const bool b1 = cf >= e01.y, b2 = cf >= e23.x, b3 = cf >= e23.y;
+            uint32_t cum = b3 ? e23.y : (b2 ? e23.x : (b1 ? e01.y : e01.x));
+            uint32_t nxt = b3 ? e4s.x : (b2 ? e23.y : (b1 ? e23.x : e01.y));
+            uint32_t sx = e4s.y + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
+            const bool far = cf >= e4s.x;
+            if (__builtin_expect(__any(far), 0)) {  // four or more boundaries in the bucket
+                if (far) {
+                    sx = e4s.y + 4;
+                    while (cf >= lcum[sx + 1]) ++sx;
+                    cum = lcum[sx];
+                    nxt = lcum[sx + 1];
                 }
             }
-            head = q * mass + (cf - cum);  // src/ans.rs:113-114
+            head = qq * (nxt - cum) + (cf - cum);  // src/ans.rs:113-114
             put_sym<Sym>(outv, j, sx);
         }
         switch (u & 3) {
@@ -411,10 +410,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
         d[2] = q2;
         d[3] = q3;
     }
-
     // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
-    for (int g = 0; g < 9 && head < kMaxMinHead; ++g) head = pull1(head);
-    const int32_t remaining = 4 * (nd_idx + 1) + static_cast<int32_t>(nW);  // < 0: generated bytes used
+    for (int g = 0; g < 9 && head < kMaxMinHead; ++g) {
+        if (nW == 0) refill();
+        head = (head << 8) | (w1 >> 24);
+        w1 = ab(w1, w0, 3);
+        w0 <<= 8;
+        nW -= 1;
+    }
+    const int32_t remaining = 4 * (nd_idx + 1) + static_cast<int32_t>(nW);  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }

@@ -442,46 +442,46 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         for (uint32_t j = 1; j <= 4; ++j)  // can a push emit j bytes? (head < 2^64 <= p*K*2^8j otherwise)
             if ((pK << (8 * j)) < (static_cast<u128>(1) << 64) && j > kmax) kmax = j;
     }
-    uint32_t bits = 0;
-    while (bits < 32 && (1ull << bits) < t.norm) ++bits;
-    ft.shift8 = bits > 13 ? bits - 13 : 0;  // <= 8192 one-byte buckets
-    const uint64_t width = 1ull << ft.shift8;
-    std::vector<DecRow> dec(nsym + 3, DecRow{t.norm, 0});
-    for (uint32_t s = 0; s < nsym; ++s) {
-        const uint64_t m1 = s + 1 < nsym ? cat.masses[s + 1] : width;
-        const uint64_t m2 = s + 2 < nsym ? cat.masses[s + 2] : width;
-        const bool multi = m1 + m2 < width;  // a bucket from s could reach past cum[s+3]
-        dec[s] = DecRow{static_cast<uint32_t>(cat.cummasses[s]),
-                        static_cast<uint32_t>(cat.masses[s]) | (multi ? kDecMulti : 0u)};
+    // decode buckets: the finest power-of-two width whose table fits fast::kDecTableBytes
+    uint32_t shift = 0;
+    const size_t cum_bytes = sizeof(uint32_t) * (nsym + 5);
+    while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > (fast::kDecTableBytes - cum_bytes) / sizeof(DecBucket))
+        ++shift;
+    const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1);
+    std::vector<uint32_t> cum(nsym + 5, t.norm);
+    for (uint32_t s = 0; s < nsym; ++s) cum[s] = static_cast<uint32_t>(cat.cummasses[s]);
+    std::vector<DecBucket> dec(nb);
+    for (uint32_t j = 0; j < nb; ++j) {
+        const uint32_t s0 = static_cast<uint32_t>(cat.icdf(static_cast<uint64_t>(j) << shift).first);
+        DecBucket& d = dec[j];
+        for (int i = 0; i < 5; ++i) d.c[i] = cum[s0 + i];
+        d.s0 = s0;
     }
-    const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(t.norm) + width - 1) >> ft.shift8);
-    ft.bucket_lds_bytes = (nb + 15) & ~15u;
-    std::vector<uint8_t> bucket(ft.bucket_lds_bytes, 0);
-    for (uint32_t j = 0; j < nb; ++j)
-        bucket[j] = static_cast<uint8_t>(cat.icdf(static_cast<uint64_t>(j) << ft.shift8).first);
     ft.nsym = nsym;
     ft.enc_rows = nsym + 1;
-    ft.dec_rows = nsym + 3;
+    ft.dec_buckets = nb;
+    ft.dec_shift = shift;
     ft.norm = t.norm;
     ft.enc_lds_bytes = static_cast<uint32_t>((sizeof(EncRow) * enc.size() + 15) & ~size_t(15));
-    ft.dec_lds_bytes = ft.bucket_lds_bytes + static_cast<uint32_t>((sizeof(DecRow) * dec.size() + 15) & ~size_t(15));
+    ft.dec_cum_off = static_cast<uint32_t>((sizeof(DecBucket) * dec.size() + 15) & ~size_t(15));
+    ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;
     ft.K = t.K;
     ft.L = t.L;
     ft.rcp_norm = t.rcp_norm;
-    const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = sizeof(DecRow) * dec.size();
-    const size_t o_dec = (enc_b + 255) & ~size_t(255), o_bkt = o_dec + ((dec_b + 255) & ~size_t(255));
+    const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = sizeof(DecBucket) * dec.size();
+    const size_t o_dec = (enc_b + 255) & ~size_t(255), o_cum = o_dec + ((dec_b + 255) & ~size_t(255));
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
-    HIP_TRY(hipMalloc(&mem, o_bkt + bucket.size()));
+    HIP_TRY(hipMalloc(&mem, o_cum + sizeof(uint32_t) * cum.size()));
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_dec, dec.data(), dec_b, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(base + o_bkt, bucket.data(), bucket.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_cum, cum.data(), sizeof(uint32_t) * cum.size(), hipMemcpyHostToDevice));
     ft.enc = reinterpret_cast<const EncRow*>(base);
-    ft.dec = reinterpret_cast<const DecRow*>(base + o_dec);
-    ft.bucket8 = reinterpret_cast<const uint8_t*>(base + o_bkt);
+    ft.dbkt = reinterpret_cast<const DecBucket*>(base + o_dec);
+    ft.cum = reinterpret_cast<const uint32_t*>(base + o_cum);
     ft.usable = 1;
     gt->ft = ft;
     return ANS_OK;

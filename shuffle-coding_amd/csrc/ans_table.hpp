@@ -50,28 +50,27 @@ struct EncRow {
     uint32_t mass;
     uint32_t cum;
 };
-// Decode row (8 B): symbol s covers cdf values [cum, cum + mass); row nsym is the sentinel
-// {norm, 0}.  Bit 31 of `mass` flags that a bucket starting in this symbol may contain
-// three or more cdf boundaries (rows s+1 and s+2 narrower than one bucket together).
-struct DecRow {
-    uint32_t cum;
-    uint32_t mass;
+// Decode bucket (24 B, three ds_read_b64): bucket j covers cdf values [j << dec_shift,
+// (j+1) << dec_shift).  s0 = icdf(j << dec_shift) and c[i] = cdf(s0 + i), i = 0..4 (norm past
+// the last symbol), so one LDS round trip resolves every cf in the bucket below c[4]; the
+// rest (a bucket holding four or more boundaries) scan the cdf table staged after the buckets.
+struct alignas(8) DecBucket {
+    uint32_t c[5];
+    uint32_t s0;
 };
-constexpr uint32_t kDecMulti = 0x80000000u;
 struct FastTable {
-    const EncRow* enc;       // enc_rows = nsym + 1 rows (last = zero-mass sentinel)
-    const DecRow* dec;       // nsym + 3 rows (sentinels) so s0 + 2 is always readable
-    const uint8_t* bucket8;  // bucket8[j] = icdf(j << shift8).x, padded to bucket_lds_bytes
+    const EncRow* enc;        // enc_rows = nsym + 1 rows (last = zero-mass sentinel)
+    const DecBucket* dbkt;    // dec_buckets entries
+    const uint32_t* cum;      // cdf(s) for s = 0..nsym+4 (norm from nsym on): the slow icdf path
     uint32_t nsym;
     uint32_t enc_rows;
-    uint32_t dec_rows;
+    uint32_t dec_buckets;
     uint32_t norm;
-    uint32_t shift8;
-    uint32_t enc_lds_bytes;     // LDS bytes of the staged encode rows (16-aligned)
-    uint32_t bucket_lds_bytes;  // LDS bytes of the staged buckets (16-aligned)
-    uint32_t dec_lds_bytes;     // buckets + decode rows (16-aligned)
-    uint32_t kmax;              // max bytes one push emits (1..4)
-    uint32_t pad;
+    uint32_t dec_shift;
+    uint32_t enc_lds_bytes;   // LDS bytes of the staged encode rows (16-aligned)
+    uint32_t dec_lds_bytes;   // LDS bytes of the staged decode buckets + cdf table (16-aligned)
+    uint32_t dec_cum_off;     // LDS offset of the cdf table
+    uint32_t kmax;            // max bytes one push (and so one pop) moves (1..4)
     uint64_t K;
     uint64_t L;
     double rcp_norm;
