@@ -18,6 +18,7 @@ cpu_baseline: the oracle (oracle/ans_oracle.c, single thread) timed on a bounded
 sample of the same workload (rank 0, N=1 only).
 """
 import argparse
+import glob
 import hashlib
 import json
 import os
@@ -63,16 +64,24 @@ def lib_hash():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(kernel_key, n_launch_bytes_hint):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary of THIS library build
-    (profiles/pmc_<libhash>.json, written by tools/pmc_summary.py), else None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{lib_hash()}.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    k = d.get("kernels", {}).get(kernel_key)
-    return None if k is None else k.get("hbm_bytes_per_launch")
+def pmc_traffic(kernel_key, config, log2n, chunk_len):
+    """HBM bytes per launch of `kernel_key` from a committed rocprofv3 PMC summary of the
+    same workload (profiles/*pmc*.json, written by tools/pmc_summary.py --json), preferring
+    one taken on this exact library build; (bytes, source file) or (None, None)."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel_key)
+        if k is None or (d.get("config"), d.get("log2n"), d.get("chunk_len")) != (config, log2n, chunk_len):
+            continue
+        rank = (d.get("lib_hash") == lib_hash(), path)
+        if best is None or rank > best[0]:
+            best = (rank, k.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT))
+    return (None, None) if best is None else (best[1], best[2])
 
 
 def cpu_baseline(masses, sym_bytes, seed, chunk_len, target_s):
@@ -183,7 +192,7 @@ def main():
     alg_bytes = n * sym_bytes + comp_bytes  # per launch, encode and decode alike
     dom_name, dom_ms = ("decode", dec_ms) if dec_ms >= enc_ms else ("encode", enc_ms)
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(f"k_{dom_name}", alg_bytes)
+    traffic, traffic_src = pmc_traffic(f"k_{dom_name}", args.config, log2n, L)
 
     if rank == 0:
         line = {
@@ -221,7 +230,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_src": traffic_src,
             },
         }
         if world == 1 and not args.no_cpu_baseline:

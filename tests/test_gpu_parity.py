@@ -95,6 +95,19 @@ def test_random_tables_bit_exact(gpu, nsym, lo, hi, zero_frac, chunk_len, n):
         _roundtrip_vs_oracle(gpu, masses, syms, chunk_len, dtype)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_fast_decoder_crowded_buckets(gpu, seed):
+    """Hundreds of cdf boundaries inside one decode bucket (the bucket table resolves four;
+    the rest scan the staged cdf table), symbols drawn uniformly so those are hit often."""
+    rng = np.random.default_rng(seed)
+    masses = np.ones(256, np.uint64)
+    masses[rng.choice(256, 6, replace=False)] = 1 << 22
+    masses[rng.choice(256, 40, replace=False)] += rng.integers(0, 2000, 40).astype(np.uint64)
+    syms = rng.integers(0, 256, size=520 * 4096 + 99).astype(np.uint32)
+    for dtype in (np.uint8, np.uint16, np.uint32):
+        _roundtrip_vs_oracle(gpu, masses, syms, 4096, dtype)
+
+
 def test_ragged_and_empty_inputs(gpu):
     masses = [5, 9, 1, 300000, 17]
     rng = np.random.default_rng(5)

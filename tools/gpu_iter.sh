@@ -16,6 +16,6 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpur
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${TAG}_bench.log
 [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_${TAG}.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof_${TAG}.log 2>&1
 rc=$?; echo "prof rc=$rc"
 cut -d, -f1-4 gpurun_out/prof_${TAG}/run_kernel_stats.csv | cut -c1-160 | head -8

@@ -3,6 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-pmc}; shift
+# PMC_META: e.g. "--config c3 --log2n 30" (recorded in pmc.json for bench.py)
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc_${TAG}
 i=0
@@ -15,4 +16,4 @@ for grp in \
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc_${TAG}/p$i -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/pmc_${TAG}/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_${TAG}/p$i.log; exit $rc; }
 done
-python3 tools/pmc_summary.py gpurun_out/pmc_${TAG} | tee gpurun_out/pmc_${TAG}/summary.txt
+python3 tools/pmc_summary.py gpurun_out/pmc_${TAG} --json gpurun_out/pmc_${TAG}/pmc.json ${PMC_META} | tee gpurun_out/pmc_${TAG}/summary.txt
