@@ -232,16 +232,160 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
 }
 
 // ====================================================================== decode
-// The lane's stream pages land in its ring at points: page low+1 is consumed once the next
-// dword to read (nd_idx) lies below it, and the page below `low` is always in flight in
-// registers (S), so after a point the ring holds at least 16 unread dwords.  One unit pops
-// U symbols of at most KMAX <= 4 bytes each, <= 64 bytes = 16 dwords: no lane can run dry
-// between points, and the step needs no availability test.
-template <typename Sym>
-__global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
-                                                      const uint32_t* __restrict__ lens, uint64_t chunk_len,
-                                                      uint64_t nfull, int gen_kind, Sym* __restrict__ out,
-                                                      uint32_t* __restrict__ status) {
+// One decode chain = one chunk.  Its stream pages land in a lane-private ring at points: page
+// low+1 is consumed once the next dword to read (nd_idx) lies below it, and the page below
+// `low` is always in flight in registers (S), so after a point the ring holds at least 16
+// unread dwords.  One unit pops U symbols of at most KMAX <= 4 bytes each, <= 64 bytes = 16
+// dwords: no chain can run dry between points, and a step needs no availability test.
+template <int kStride>  // dwords between consecutive ring slots of one chain
+struct DecChain {
+    uint32_t* ring;  // &image[0][chain][lane]
+    const uint8_t* src;
+    uint4 S[4];
+    int32_t low, nd_idx;
+    bool pend;
+    uint32_t w1, w0, nW, nd;  // window: nW stream bytes MSB-aligned in (w1:w0); nd = dword nd_idx
+    uint64_t head;
+    // per-step values between the phases
+    uint64_t qq;
+    uint32_t cf, cum, nxt, sx;
+    bool far;
+
+    __device__ __forceinline__ uint32_t& at(int32_t i) const { return ring[(static_cast<uint32_t>(i) & 31u) * kStride]; }
+    __device__ __forceinline__ void put_page(int32_t p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            at(16 * p + 4 * k + 0) = S[k].x;
+            at(16 * p + 4 * k + 1) = S[k].y;
+            at(16 * p + 4 * k + 2) = S[k].z;
+            at(16 * p + 4 * k + 3) = S[k].w;
+        }
+    }
+    __device__ __forceinline__ void fetch_page(int32_t p) {
+        const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) S[k] = g[k];
+    }
+    // the top two pages land before decoding starts; the third is requested
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
+        src = s;
+        const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
+        low = top;
+        if (len > 0) {
+            fetch_page(top);
+            wait_vm();
+            put_page(top);
+        }
+        if (top >= 1) {
+            fetch_page(top - 1);
+            wait_vm();
+            put_page(top - 1);
+            low = top - 1;
+        }
+        pend = low >= 1;
+        if (pend) fetch_page(low - 1);
+        w1 = w0 = nW = 0;
+        nd_idx = -1;
+        if (len > 0) {
+            const int32_t td = (len - 1) >> 2;
+            const uint32_t cb = static_cast<uint32_t>(len - 4 * td);
+            w1 = at(td) << (8 * (4 - cb));
+            nW = cb;
+            nd_idx = td - 1;
+        }
+        const uint32_t v = at(nd_idx);
+        nd = nd_idx >= 0 ? v : 0u;  // below the stream: the Zeros generator (src/ans.rs:160-170)
+        head = 0;
+    }
+    __device__ __forceinline__ void refill() {  // nd into the window when nW <= 4
+        const bool take = nW <= 4;
+        const uint64_t add = (static_cast<uint64_t>(nd) << 32) >> (8 * (nW & 7));
+        w1 = take ? (w1 | hi32(add)) : w1;
+        w0 = take ? lo32(add) : w0;
+        nW += take ? 4u : 0u;
+        nd_idx -= take ? 1 : 0;
+        const uint32_t v = at(nd_idx);
+        nd = nd_idx >= 0 ? v : 0u;
+    }
+    // renorm_up one byte at a time (unflatten and the final equality check only)
+    __device__ __forceinline__ void pull_until(uint64_t bound) {
+        for (int g = 0; g < 9 && head < bound; ++g) {
+            if (nW == 0) refill();
+            head = (head << 8) | (w1 >> 24);
+            w1 = ab(w1, w0, 3);
+            w0 <<= 8;
+            nW -= 1;
+        }
+    }
+    __device__ __forceinline__ void point() {
+        if (pend && (nd_idx >> 4) <= low) {  // page low+1 consumed: land the page below
+            put_page(low - 1);
+            --low;
+            pend = low >= 1;
+            if (pend) fetch_page(low - 1);
+        }
+    }
+    // phase 1: refill, renorm_up, q/cf
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
+        refill();
+        // renorm_up (src/ans.rs:239-243): k = min{j : top64((head:W) << 8j) >= L}.  With bl the
+        // head's bit length, js = (64 - bl) >> 3 bytes reach 2^56 >= L; js-1 may too.
+        const uint32_t h1 = hi32(head), h0 = lo32(head);
+        const uint32_t bl = 64u - static_cast<uint32_t>(__builtin_clzll(head | 1));
+        const uint32_t js = (64u - bl) >> 3;
+        const uint32_t m = js - 1;
+        const uint32_t sm = (4u - m) & 3u;
+        const uint32_t t1 = m == 0 ? h1 : ab(h1, h0, sm);
+        const uint32_t t0 = m == 0 ? h0 : ab(h0, w1, sm);
+        const uint32_t k = js - ((js >= 1 ? 1u : 0u) & (mk64(t1, t0) >= L ? 1u : 0u));
+        const uint32_t sk = (4u - k) & 3u;
+        const bool nz = k != 0;
+        head = nz ? mk64(ab(h1, h0, sk), ab(h0, w1, sk)) : head;
+        const uint32_t x1 = ab(w1, w0, sk), x0 = ab(w0, 0u, sk);
+        w1 = nz ? x1 : w1;
+        w0 = nz ? x0 : w0;
+        nW -= k;
+        // q = head / norm, cf = head % norm (src/ans.rs:110-111)
+        uint64_t q = qest(head, rcp_norm);
+        const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
+        const uint32_t neg = ii < 0 ? 1u : 0u;
+        qq = q - neg;
+        cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
+    }
+    // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket
+    __device__ __forceinline__ void lookup(const unsigned char* bkt, uint32_t shift) {
+        const uint64_t* e = reinterpret_cast<const uint64_t*>(bkt + __umul24(cf >> shift, sizeof(DecBucket)));
+        uint64_t r01 = e[0], r23 = e[1], r4s = e[2];
+        // all three reads complete here: the compiler otherwise defers the ones a select needs
+        // only on some lanes into branches, adding dependent LDS round trips
+        asm volatile("" : "+v"(r01), "+v"(r23), "+v"(r4s));
+        const uint2 e01 = make_uint2(lo32(r01), hi32(r01)), e23 = make_uint2(lo32(r23), hi32(r23)),
+                    e4s = make_uint2(lo32(r4s), hi32(r4s));
+        const bool b1 = cf >= e01.y, b2 = cf >= e23.x, b3 = cf >= e23.y;
+        cum = b3 ? e23.y : (b2 ? e23.x : (b1 ? e01.y : e01.x));
+        nxt = b3 ? e4s.x : (b2 ? e23.y : (b1 ? e23.x : e01.y));
+        sx = e4s.y + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
+        far = cf >= e4s.x;
+    }
+    __device__ __forceinline__ void lookup_far(const uint32_t* lcum) {  // 4+ boundaries in the bucket
+        if (far) {
+            sx += 1;
+            while (cf >= lcum[sx + 1]) ++sx;
+            cum = lcum[sx];
+            nxt = lcum[sx + 1];
+        }
+    }
+    // phase 3: head = p*q + r (src/ans.rs:113-114)
+    __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
+};
+
+// NC chunks per lane (chains), interleaved phase by phase so that one chain's latencies are
+// covered by the others' work.  The ring image is [dword][chain][lane].
+template <typename Sym, int NC>
+__global__ __launch_bounds__(kBlock, NC == 1 ? 4 : 2) void k_decode(FastTable t, const uint8_t* __restrict__ slots,
+                                                                    uint64_t slot_cap, const uint32_t* __restrict__ lens,
+                                                                    uint64_t chunk_len, uint64_t nfull, int gen_kind,
+                                                                    Sym* __restrict__ out, uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
     {
         uint2* b = reinterpret_cast<uint2*>(lds);
@@ -252,175 +396,89 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     }
     const unsigned char* bkt = lds;
     const uint32_t* lcum = reinterpret_cast<const uint32_t*>(lds + t.dec_cum_off);
-    const Ring ring{reinterpret_cast<uint32_t*>(lds + t.dec_lds_bytes) + threadIdx.x};
+    uint32_t* ring0 = reinterpret_cast<uint32_t*>(lds + t.dec_lds_bytes) + threadIdx.x;
     __syncthreads();
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c >= nfull) return;
+    const uint64_t c0 = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) * NC;
+    if (c0 >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     const int nunit = static_cast<int>(chunk_len / U);
-    const uint8_t* src = slots + c * slot_cap;
-    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
-    const int32_t len = static_cast<int32_t>(lens[c]);
     const uint64_t L = t.L;
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
 
-    uint4 S[4];
-    auto put_page = [&](int32_t p) __attribute__((always_inline)) {
+    DecChain<NC * kBlock> ch[NC];
+    uint4 q[NC][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            ring.at(16 * p + 4 * k + 0) = S[k].x;
-            ring.at(16 * p + 4 * k + 1) = S[k].y;
-            ring.at(16 * p + 4 * k + 2) = S[k].z;
-            ring.at(16 * p + 4 * k + 3) = S[k].w;
-        }
-    };
-    auto fetch_page = [&](int32_t p) __attribute__((always_inline)) {
-        const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) S[k] = g[k];
-    };
-
-    // the top two pages land before decoding starts; the third is requested
-    const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
-    int32_t low = top;
-    if (len > 0) {
-        fetch_page(top);
-        wait_vm();
-        put_page(top);
-    }
-    if (top >= 1) {
-        fetch_page(top - 1);
-        wait_vm();
-        put_page(top - 1);
-        low = top - 1;
-    }
-    bool pend = low >= 1;
-    if (pend) fetch_page(low - 1);
-
-    // window: (w1:w0) holds nW stream bytes MSB-aligned (next byte to pop on top);
-    // nd = stream dword nd_idx, the next one below the window (0 below the stream: the
-    // Zeros generator, src/ans.rs:160-170).
-    uint32_t w1 = 0, w0 = 0, nW = 0;
-    int32_t nd_idx = -1;
-    if (len > 0) {
-        const int32_t td = (len - 1) >> 2;
-        const uint32_t cb = static_cast<uint32_t>(len - 4 * td);
-        w1 = ring.at(td) << (8 * (4 - cb));
-        nW = cb;
-        nd_idx = td - 1;
-    }
-    uint32_t nd = ring.at(nd_idx);
-    nd = nd_idx >= 0 ? nd : 0u;
-    auto refill = [&]() __attribute__((always_inline)) {  // nd into the window when nW <= 4
-        const bool take = nW <= 4;
-        const uint64_t add = (static_cast<uint64_t>(nd) << 32) >> (8 * (nW & 7));
-        w1 = take ? (w1 | hi32(add)) : w1;
-        w0 = take ? lo32(add) : w0;
-        nW += take ? 4u : 0u;
-        nd_idx -= take ? 1 : 0;
-        const uint32_t v = ring.at(nd_idx);
-        nd = nd_idx >= 0 ? v : 0u;
-    };
-    uint64_t head = 0;  // Message::unflatten: head 0, then renorm_up pulls the flushed head
-    for (int g = 0; g < 9 && head < L; ++g) {
-        if (nW == 0) refill();
-        head = (head << 8) | (w1 >> 24);
-        w1 = ab(w1, w0, 3);
-        w0 <<= 8;
-        nW -= 1;
+    for (int i = 0; i < NC; ++i) {
+        ch[i].ring = ring0 + i * kBlock;
+        ch[i].start(slots + (c0 + i) * slot_cap, static_cast<int32_t>(lens[c0 + i]));
+        ch[i].pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
     }
 
-    uint4 q0, q1, q2, q3;
     for (int u = 0; u < nunit; ++u) {
         wait_vm();  // point: retire what the previous point issued
-        if (u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
-            uint4* d = dst + (u - 4);
-            d[0] = q0;
-            d[1] = q1;
-            d[2] = q2;
-            d[3] = q3;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            if (u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
+                uint4* d = reinterpret_cast<uint4*>(out + (c0 + i) * chunk_len) + (u - 4);
+                d[0] = q[i][0];
+                d[1] = q[i][1];
+                d[2] = q[i][2];
+                d[3] = q[i][3];
+            }
+            ch[i].point();
         }
-        if (pend && (nd_idx >> 4) <= low) {  // page low+1 consumed: land the page below
-            put_page(low - 1);
-            --low;
-            pend = low >= 1;
-            if (pend) fetch_page(low - 1);
-        }
-        uint4 outv = make_uint4(0, 0, 0, 0);
+        uint4 outv[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) outv[i] = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            refill();
-            // renorm_up (src/ans.rs:239-243): k = min{j : top64((head:W) << 8j) >= L}.  With
-            // bl the head's bit length, js = (64 - bl) >> 3 bytes reach 2^56 >= L; js-1 may too.
-            const uint32_t h1 = hi32(head), h0 = lo32(head);
-            const uint32_t bl = 64u - static_cast<uint32_t>(__builtin_clzll(head | 1));
-            const uint32_t js = (64u - bl) >> 3;
-            const uint32_t m = js - 1;
-            const uint32_t sm = (4u - m) & 3u;
-            const uint32_t t1 = m == 0 ? h1 : ab(h1, h0, sm);
-            const uint32_t t0 = m == 0 ? h0 : ab(h0, w1, sm);
-            const uint32_t k = js - ((js >= 1 ? 1u : 0u) & (mk64(t1, t0) >= L ? 1u : 0u));
-            const uint32_t sk = (4u - k) & 3u;
-            const bool nz = k != 0;
-            head = nz ? mk64(ab(h1, h0, sk), ab(h0, w1, sk)) : head;
-            const uint32_t x1 = ab(w1, w0, sk), x0 = ab(w0, 0u, sk);
-            w1 = nz ? x1 : w1;
-            w0 = nz ? x0 : w0;
-            nW -= k;
-            // q = head / norm, cf = head % norm (src/ans.rs:110-111)
-            uint64_t qq = qest(head, rcp_norm);
-            const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(qq) * norm);
-            const uint32_t neg = ii < 0 ? 1u : 0u;
-            qq -= neg;
-            const uint32_t cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
-            // icdf (src/codec.rs:65-68): the last symbol with cdf <= cf, from cf's bucket
-            const uint2* e = reinterpret_cast<const uint2*>(bkt + __umul24(cf >> shift, sizeof(DecBucket)));
-            const uint2 e01 = e[0], e23 = e[1], e4s = e[2];
-            const bool b1 = cf >= e01.y, b2 = cf >= e23.x, b3 = cf >= e23.y;
-            uint32_t cum = b3 ? e23.y : (b2 ? e23.x : (b1 ? e01.y : e01.x));
-            uint32_t nxt = b3 ? e4s.x : (b2 ? e23.y : (b1 ? e23.x : e01.y));
-            uint32_t sx = e4s.y + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
-            const bool far = cf >= e4s.x;
-            if (__builtin_expect(__any(far), 0)) {  // four or more boundaries in the bucket
-                if (far) {
-                    sx = e4s.y + 4;
-                    while (cf >= lcum[sx + 1]) ++sx;
-                    cum = lcum[sx];
-                    nxt = lcum[sx + 1];
-                }
+#pragma unroll
+            for (int i = 0; i < NC; ++i) ch[i].renorm_div(L, norm, rcp_norm);
+            bool far = false;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                ch[i].lookup(bkt, shift);
+                far |= ch[i].far;
             }
-            head = qq * (nxt - cum) + (cf - cum);  // src/ans.rs:113-114
-            put_sym<Sym>(outv, j, sx);
+            if (__builtin_expect(__any(far), 0)) {
+#pragma unroll
+                for (int i = 0; i < NC; ++i) ch[i].lookup_far(lcum);
+            }
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                ch[i].update();
+                put_sym<Sym>(outv[i], j, ch[i].sx);
+            }
         }
-        switch (u & 3) {
-        case 0: q0 = outv; break;
-        case 1: q1 = outv; break;
-        case 2: q2 = outv; break;
-        default: q3 = outv; break;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            switch (u & 3) {
+            case 0: q[i][0] = outv[i]; break;
+            case 1: q[i][1] = outv[i]; break;
+            case 2: q[i][2] = outv[i]; break;
+            default: q[i][3] = outv[i]; break;
+            }
         }
     }
     wait_vm();
-    if (nunit >= 4) {
-        uint4* d = dst + (nunit - 4);
-        d[0] = q0;
-        d[1] = q1;
-        d[2] = q2;
-        d[3] = q3;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        if (nunit >= 4) {
+            uint4* d = reinterpret_cast<uint4*>(out + (c0 + i) * chunk_len) + (nunit - 4);
+            d[0] = q[i][0];
+            d[1] = q[i][1];
+            d[2] = q[i][2];
+            d[3] = q[i][3];
+        }
+        // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
+        ch[i].pull_until(kMaxMinHead);
+        const int32_t remaining = 4 * (ch[i].nd_idx + 1) + static_cast<int32_t>(ch[i].nW);  // < 0: generated
+        if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
+        else if (ch[i].head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
     }
-    // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
-    for (int g = 0; g < 9 && head < kMaxMinHead; ++g) {
-        if (nW == 0) refill();
-        head = (head << 8) | (w1 >> 24);
-        w1 = ab(w1, w0, 3);
-        w0 <<= 8;
-        nW -= 1;
-    }
-    const int32_t remaining = 4 * (nd_idx + 1) + static_cast<int32_t>(nW);  // < 0: generated
-    if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
-    else if (head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
 
 }  // namespace fast
