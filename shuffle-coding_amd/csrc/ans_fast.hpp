@@ -31,7 +31,7 @@ namespace fast {
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
-constexpr uint32_t kDecTableBytes = 16384;  // decode buckets in LDS: 2 x (64 KiB ring + 16 KiB) per CU
+constexpr uint32_t kDecTableBytes = 14336;  // decode buckets in LDS: 2 x (66 KiB ring + 14 KiB) per CU
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
@@ -232,119 +232,103 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
 }
 
 // ====================================================================== decode
-// One decode chain = one chunk.  Its stream pages land in a lane-private ring at points: page
-// low+1 is consumed once the next dword to read (nd_idx) lies below it, and the page below
-// `low` is always in flight in registers (S), so after a point the ring holds at least 16
-// unread dwords.  One unit pops U symbols of at most KMAX <= 4 bytes each, <= 64 bytes = 16
-// dwords: no chain can run dry between points, and a step needs no availability test.
-template <int kStride>  // dwords between consecutive ring slots of one chain
+// One decode chain = one chunk, read from the end.  P is the stream position minus 4: the
+// window W = stream bytes [P, P+4) (byte P+3 on top) comes from ring dwords y = P>>2 and y+1
+// with one v_alignbyte.  The ring (LDS offset 0) is [row][lane] with kDecRows = 33 rows:
+// row 32 mirrors row 0, so y and y+1 are one ds_read2st64_b32 even across the wrap.  Pages
+// (16 rows) land at points: page low+1 is free once dword y+1 lies in page low, and the page
+// below `low` is always in flight in registers (S); pages below 0 are zeros (the Zeros
+// generator, src/ans.rs:160-170).  A point covers at most 60 stream bytes (SPP symbols of at
+// most KMAX bytes), so no read between points can reach an unlanded page.
+constexpr int kDecRows = 33;
+constexpr uint32_t kDecRingBytes = kDecRows * kBlock * 4;
+
 struct DecChain {
-    uint32_t* ring;  // &image[0][chain][lane]
+    uint32_t* ring;  // &ring[0][lane]
     const uint8_t* src;
     uint4 S[4];
-    int32_t low, nd_idx;
-    bool pend;
-    uint32_t w1, w0, nW, nd;  // window: nW stream bytes MSB-aligned in (w1:w0); nd = dword nd_idx
+    int32_t low, P;
+    uint32_t W;
     uint64_t head;
     // per-step values between the phases
     uint64_t qq;
     uint32_t cf, cum, nxt, sx;
     bool far;
 
-    __device__ __forceinline__ uint32_t& at(int32_t i) const { return ring[(static_cast<uint32_t>(i) & 31u) * kStride]; }
+    __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kBlock]; }
     __device__ __forceinline__ void put_page(int32_t p) {
+        const int32_t r0 = (p & 1) * 16;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            at(16 * p + 4 * k + 0) = S[k].x;
-            at(16 * p + 4 * k + 1) = S[k].y;
-            at(16 * p + 4 * k + 2) = S[k].z;
-            at(16 * p + 4 * k + 3) = S[k].w;
+            row(r0 + 4 * k + 0) = S[k].x;
+            row(r0 + 4 * k + 1) = S[k].y;
+            row(r0 + 4 * k + 2) = S[k].z;
+            row(r0 + 4 * k + 3) = S[k].w;
         }
+        if ((p & 1) == 0) row(32) = S[0].x;
     }
     __device__ __forceinline__ void fetch_page(int32_t p) {
-        const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
+        if (p >= 0) {
+            const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) S[k] = g[k];
+            for (int k = 0; k < 4; ++k) S[k] = g[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S[k] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0)
+    __device__ __forceinline__ void read_window() {
+        const uint32_t* a = ring + ((static_cast<uint32_t>(P) >> 2) & 31u) * kBlock;
+        const uint32_t y = a[0], x = a[kBlock];
+        W = ab(x, y, static_cast<uint32_t>(P) & 3u);
     }
     // the top two pages land before decoding starts; the third is requested
     __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
         src = s;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
-        low = top;
-        if (len > 0) {
-            fetch_page(top);
-            wait_vm();
-            put_page(top);
-        }
-        if (top >= 1) {
-            fetch_page(top - 1);
-            wait_vm();
-            put_page(top - 1);
-            low = top - 1;
-        }
-        pend = low >= 1;
-        if (pend) fetch_page(low - 1);
-        w1 = w0 = nW = 0;
-        nd_idx = -1;
-        if (len > 0) {
-            const int32_t td = (len - 1) >> 2;
-            const uint32_t cb = static_cast<uint32_t>(len - 4 * td);
-            w1 = at(td) << (8 * (4 - cb));
-            nW = cb;
-            nd_idx = td - 1;
-        }
-        const uint32_t v = at(nd_idx);
-        nd = nd_idx >= 0 ? v : 0u;  // below the stream: the Zeros generator (src/ans.rs:160-170)
+        fetch_page(len > 0 ? top : -1);
+        wait_vm();
+        put_page(top);
+        fetch_page(top - 1);
+        wait_vm();
+        put_page(top - 1);
+        low = top - 1;
+        fetch_page(low - 1);
+        P = len - 4;
+        read_window();
         head = 0;
-    }
-    __device__ __forceinline__ void refill() {  // nd into the window when nW <= 4
-        const bool take = nW <= 4;
-        const uint64_t add = (static_cast<uint64_t>(nd) << 32) >> (8 * (nW & 7));
-        w1 = take ? (w1 | hi32(add)) : w1;
-        w0 = take ? lo32(add) : w0;
-        nW += take ? 4u : 0u;
-        nd_idx -= take ? 1 : 0;
-        const uint32_t v = at(nd_idx);
-        nd = nd_idx >= 0 ? v : 0u;
     }
     // renorm_up one byte at a time (unflatten and the final equality check only)
     __device__ __forceinline__ void pull_until(uint64_t bound) {
         for (int g = 0; g < 9 && head < bound; ++g) {
-            if (nW == 0) refill();
-            head = (head << 8) | (w1 >> 24);
-            w1 = ab(w1, w0, 3);
-            w0 <<= 8;
-            nW -= 1;
+            head = (head << 8) | (W >> 24);
+            P -= 1;
+            read_window();
         }
     }
     __device__ __forceinline__ void point() {
-        if (pend && (nd_idx >> 4) <= low) {  // page low+1 consumed: land the page below
+        if ((((P >> 2) + 1) >> 4) <= low) {  // page low+1 is no longer read: land the one below
             put_page(low - 1);
             --low;
-            pend = low >= 1;
-            if (pend) fetch_page(low - 1);
+            fetch_page(low - 1);
         }
     }
-    // phase 1: refill, renorm_up, q/cf
+    // phase 1: renorm_up, q/cf, next window
     __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
-        refill();
-        // renorm_up (src/ans.rs:239-243): k = min{j : top64((head:W) << 8j) >= L}.  With bl the
-        // head's bit length, js = (64 - bl) >> 3 bytes reach 2^56 >= L; js-1 may too.
+        // renorm_up (src/ans.rs:239-243) pulls k bytes: with js = clz(head) >> 3, (h:W) >> (32-8js)
+        // is >= 2^56 >= L, and k = js - 1 suffices iff that value >> 8 is >= L already.
         const uint32_t h1 = hi32(head), h0 = lo32(head);
-        const uint32_t bl = 64u - static_cast<uint32_t>(__builtin_clzll(head | 1));
-        const uint32_t js = (64u - bl) >> 3;
-        const uint32_t m = js - 1;
-        const uint32_t sm = (4u - m) & 3u;
-        const uint32_t t1 = m == 0 ? h1 : ab(h1, h0, sm);
-        const uint32_t t0 = m == 0 ? h0 : ab(h0, w1, sm);
-        const uint32_t k = js - ((js >= 1 ? 1u : 0u) & (mk64(t1, t0) >= L ? 1u : 0u));
-        const uint32_t sk = (4u - k) & 3u;
-        const bool nz = k != 0;
-        head = nz ? mk64(ab(h1, h0, sk), ab(h0, w1, sk)) : head;
-        const uint32_t x1 = ab(w1, w0, sk), x0 = ab(w0, 0u, sk);
-        w1 = nz ? x1 : w1;
-        w0 = nz ? x0 : w0;
-        nW -= k;
+        const uint32_t js = static_cast<uint32_t>(__builtin_clzll(head | 1)) >> 3;
+        const uint32_t sh = 4u - js;  // js in 1..4 here; js = 0 (head >= 2^56) is kept below
+        const uint32_t xj1 = ab(h1, h0, sh), xj0 = ab(h0, W, sh);
+        const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
+        const bool one_less = mk64(xm1, xm0) >= L;
+        const bool keep = h1 >= (1u << 24);
+        const uint32_t k = keep ? 0u : js - (one_less ? 1u : 0u);
+        head = keep ? head : (one_less ? mk64(xm1, xm0) : mk64(xj1, xj0));
+        P -= static_cast<int32_t>(k);
+        read_window();
         // q = head / norm, cf = head % norm (src/ans.rs:110-111)
         uint64_t q = qest(head, rcp_norm);
         const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
@@ -379,106 +363,82 @@ struct DecChain {
     __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
 };
 
-// NC chunks per lane (chains), interleaved phase by phase so that one chain's latencies are
-// covered by the others' work.  The ring image is [dword][chain][lane].
-template <typename Sym, int NC>
-__global__ __launch_bounds__(kBlock, NC == 1 ? 4 : 2) void k_decode(FastTable t, const uint8_t* __restrict__ slots,
-                                                                    uint64_t slot_cap, const uint32_t* __restrict__ lens,
-                                                                    uint64_t chunk_len, uint64_t nfull, int gen_kind,
-                                                                    Sym* __restrict__ out, uint32_t* __restrict__ status) {
+// SPP: symbols per point (U, or U/2 when U*KMAX > 60: u8 tables whose pops can take 4 bytes).
+template <typename Sym, int SPP>
+__global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                      const uint32_t* __restrict__ lens, uint64_t chunk_len,
+                                                      uint64_t nfull, int gen_kind, Sym* __restrict__ out,
+                                                      uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
+    unsigned char* tab = lds + kDecRingBytes;
     {
-        uint2* b = reinterpret_cast<uint2*>(lds);
+        uint2* b = reinterpret_cast<uint2*>(tab);
         const uint2* gb = reinterpret_cast<const uint2*>(t.dbkt);
         for (uint32_t i = threadIdx.x; i < 3 * t.dec_buckets; i += kBlock) b[i] = gb[i];
-        uint32_t* cl = reinterpret_cast<uint32_t*>(lds + t.dec_cum_off);
+        uint32_t* cl = reinterpret_cast<uint32_t*>(tab + t.dec_cum_off);
         for (uint32_t i = threadIdx.x; i < t.nsym + 5; i += kBlock) cl[i] = t.cum[i];
     }
-    const unsigned char* bkt = lds;
-    const uint32_t* lcum = reinterpret_cast<const uint32_t*>(lds + t.dec_cum_off);
-    uint32_t* ring0 = reinterpret_cast<uint32_t*>(lds + t.dec_lds_bytes) + threadIdx.x;
+    const uint32_t* lcum = reinterpret_cast<const uint32_t*>(tab + t.dec_cum_off);
     __syncthreads();
-    const uint64_t c0 = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) * NC;
-    if (c0 >= nfull) return;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
+    static_assert(U % SPP == 0, "points must split units evenly");
     const int nunit = static_cast<int>(chunk_len / U);
     const uint64_t L = t.L;
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
+    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
-    DecChain<NC * kBlock> ch[NC];
-    uint4 q[NC][4];
-#pragma unroll
-    for (int i = 0; i < NC; ++i) {
-        ch[i].ring = ring0 + i * kBlock;
-        ch[i].start(slots + (c0 + i) * slot_cap, static_cast<int32_t>(lens[c0 + i]));
-        ch[i].pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
-    }
+    DecChain ch;
+    ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
+    ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
+    ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 
+    uint4 q0, q1, q2, q3;
     for (int u = 0; u < nunit; ++u) {
-        wait_vm();  // point: retire what the previous point issued
-#pragma unroll
-        for (int i = 0; i < NC; ++i) {
-            if (u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
-                uint4* d = reinterpret_cast<uint4*>(out + (c0 + i) * chunk_len) + (u - 4);
-                d[0] = q[i][0];
-                d[1] = q[i][1];
-                d[2] = q[i][2];
-                d[3] = q[i][3];
-            }
-            ch[i].point();
-        }
-        uint4 outv[NC];
-#pragma unroll
-        for (int i = 0; i < NC; ++i) outv[i] = make_uint4(0, 0, 0, 0);
+        uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-#pragma unroll
-            for (int i = 0; i < NC; ++i) ch[i].renorm_div(L, norm, rcp_norm);
-            bool far = false;
-#pragma unroll
-            for (int i = 0; i < NC; ++i) {
-                ch[i].lookup(bkt, shift);
-                far |= ch[i].far;
+            if (j % SPP == 0) {
+                wait_vm();  // point: retire what the previous point issued
+                if (j == 0 && u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
+                    uint4* d = dst + (u - 4);
+                    d[0] = q0;
+                    d[1] = q1;
+                    d[2] = q2;
+                    d[3] = q3;
+                }
+                ch.point();
             }
-            if (__builtin_expect(__any(far), 0)) {
-#pragma unroll
-                for (int i = 0; i < NC; ++i) ch[i].lookup_far(lcum);
-            }
-#pragma unroll
-            for (int i = 0; i < NC; ++i) {
-                ch[i].update();
-                put_sym<Sym>(outv[i], j, ch[i].sx);
-            }
+            ch.renorm_div(L, norm, rcp_norm);
+            ch.lookup(tab, shift);
+            if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+            ch.update();
+            put_sym<Sym>(outv, j, ch.sx);
         }
-#pragma unroll
-        for (int i = 0; i < NC; ++i) {
-            switch (u & 3) {
-            case 0: q[i][0] = outv[i]; break;
-            case 1: q[i][1] = outv[i]; break;
-            case 2: q[i][2] = outv[i]; break;
-            default: q[i][3] = outv[i]; break;
-            }
+        switch (u & 3) {
+        case 0: q0 = outv; break;
+        case 1: q1 = outv; break;
+        case 2: q2 = outv; break;
+        default: q3 = outv; break;
         }
     }
     wait_vm();
-#pragma unroll
-    for (int i = 0; i < NC; ++i) {
-        if (nunit >= 4) {
-            uint4* d = reinterpret_cast<uint4*>(out + (c0 + i) * chunk_len) + (nunit - 4);
-            d[0] = q[i][0];
-            d[1] = q[i][1];
-            d[2] = q[i][2];
-            d[3] = q[i][3];
-        }
-        // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
-        ch[i].pull_until(kMaxMinHead);
-        const int32_t remaining = 4 * (ch[i].nd_idx + 1) + static_cast<int32_t>(ch[i].nW);  // < 0: generated
-        if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
-        else if (ch[i].head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+    if (nunit >= 4) {
+        uint4* d = dst + (nunit - 4);
+        d[0] = q0;
+        d[1] = q1;
+        d[2] = q2;
+        d[3] = q3;
     }
+    // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
+    ch.pull_until(kMaxMinHead);
+    const int32_t remaining = ch.P + 4;  // < 0: generated
+    if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
+    else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
 
 }  // namespace fast

@@ -370,12 +370,14 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     // the fast kernel reads the encoder's 64-byte-aligned slot layout only
     const uint64_t nfull = (d_offsets == nullptr && slot_cap % 64 == 0) ? fast_chunks<Sym>(gt, n, chunk_len) : 0;
     if (nfull) {
-        // one chain per lane: two chains per lane (k_decode<Sym, 2>) halve the waves per SIMD
-        // and measured 11% slower on C3
         const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
-        const size_t lds = ft.dec_lds_bytes + sizeof(uint32_t) * fast::kRingDwords * fast::kBlock;
-        fast::k_decode<Sym, 1><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+        const size_t lds = fast::kDecRingBytes + ft.dec_lds_bytes;
+        constexpr int U = 16 / sizeof(Sym);
+        if (U * ft.kmax > 60)
+            fast::k_decode<Sym, U / 2><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+        else
+            fast::k_decode<Sym, U><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
         HIP_TRY(hipGetLastError());
     }
     if (nfull == nchunks) return ANS_OK;
