@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
 // ====================================================================== decode
 // One decode chain = one chunk, read from the end.  P is the stream position minus 4: the
 // window W = stream bytes [P, P+4) (byte P+3 on top) comes from ring dwords y = P>>2 and y+1
-// with one v_alignbyte.  The ring (LDS offset 0) is [row][lane] with kDecRows = 33 rows:
+// with one v_alignbyte.  The ring (after the tables, at kDecTableBytes) is [row][lane] with kDecRows = 33 rows:
 // row 32 mirrors row 0, so y and y+1 are one ds_read2st64_b32 even across the wrap.  Pages
 // (16 rows) land at points: page low+1 is free once dword y+1 lies in page low, and the page
 // below `low` is always in flight in registers (S); pages below 0 are zeros (the Zeros
@@ -278,11 +278,13 @@ struct DecChain {
         }
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0)
+    uint32_t wx, wy;
     __device__ __forceinline__ void read_window() {
         const uint32_t* a = ring + ((static_cast<uint32_t>(P) >> 2) & 31u) * kBlock;
-        const uint32_t y = a[0], x = a[kBlock];
-        W = ab(x, y, static_cast<uint32_t>(P) & 3u);
+        wy = a[0];
+        wx = a[kBlock];
     }
+    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P) & 3u); }
     // the top two pages land before decoding starts; the third is requested
     __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
         src = s;
@@ -302,6 +304,7 @@ struct DecChain {
     // renorm_up one byte at a time (unflatten and the final equality check only)
     __device__ __forceinline__ void pull_until(uint64_t bound) {
         for (int g = 0; g < 9 && head < bound; ++g) {
+            form_window();
             head = (head << 8) | (W >> 24);
             P -= 1;
             read_window();
@@ -318,6 +321,7 @@ struct DecChain {
     __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
         // renorm_up (src/ans.rs:239-243) pulls k bytes: with js = clz(head) >> 3, (h:W) >> (32-8js)
         // is >= 2^56 >= L, and k = js - 1 suffices iff that value >> 8 is >= L already.
+        form_window();
         const uint32_t h1 = hi32(head), h0 = lo32(head);
         const uint32_t js = static_cast<uint32_t>(__builtin_clzll(head | 1)) >> 3;
         const uint32_t sh = 4u - js;  // js in 1..4 here; js = 0 (head >= 2^56) is kept below
@@ -328,7 +332,8 @@ struct DecChain {
         const uint32_t k = keep ? 0u : js - (one_less ? 1u : 0u);
         head = keep ? head : (one_less ? mk64(xm1, xm0) : mk64(xj1, xj0));
         P -= static_cast<int32_t>(k);
-        read_window();
+        read_window();  // for the next step; kept ahead of this step's bucket reads
+        __builtin_amdgcn_sched_barrier(0);
         // q = head / norm, cf = head % norm (src/ans.rs:110-111)
         uint64_t q = qest(head, rcp_norm);
         const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
@@ -342,7 +347,7 @@ struct DecChain {
         uint64_t r01 = e[0], r23 = e[1], r4s = e[2];
         // all three reads complete here: the compiler otherwise defers the ones a select needs
         // only on some lanes into branches, adding dependent LDS round trips
-        asm volatile("" : "+v"(r01), "+v"(r23), "+v"(r4s));
+        asm volatile("" ::"v"(r01), "v"(r23), "v"(r4s));
         const uint2 e01 = make_uint2(lo32(r01), hi32(r01)), e23 = make_uint2(lo32(r23), hi32(r23)),
                     e4s = make_uint2(lo32(r4s), hi32(r4s));
         const bool b1 = cf >= e01.y, b2 = cf >= e23.x, b3 = cf >= e23.y;
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
                                                       uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
-    unsigned char* tab = lds + kDecRingBytes;
+    unsigned char* tab = lds;  // tables at offset 0 (immediate ds offsets), ring after
     {
         uint2* b = reinterpret_cast<uint2*>(tab);
         const uint2* gb = reinterpret_cast<const uint2*>(t.dbkt);
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
     DecChain ch;
-    ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
+    ch.ring = reinterpret_cast<uint32_t*>(lds + kDecTableBytes) + threadIdx.x;
     ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 

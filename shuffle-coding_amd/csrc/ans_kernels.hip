@@ -372,7 +372,7 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     if (nfull) {
         const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
-        const size_t lds = fast::kDecRingBytes + ft.dec_lds_bytes;
+        const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
         constexpr int U = 16 / sizeof(Sym);
         if (U * ft.kmax > 60)
             fast::k_decode<Sym, U / 2><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);

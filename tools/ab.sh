@@ -2,7 +2,7 @@
 # usage: bash tools/ab.sh VAR "v1 v2 ..." [pytest -k expr]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-VAR=$1; VALS=$2; K=${3:-"crowded or random_tables or fast_kernel or golden or multiset"}
+VAR=$1; VALS=$2; K=${3:-"crowded or random_tables or fast_kernel or golden or multiset or c3"}
 mkdir -p gpurun_out
 for v in $VALS; do
   export $VAR=$v
