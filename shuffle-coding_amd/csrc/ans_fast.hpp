@@ -170,14 +170,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
             if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
             f.push<KMAX>(lo32(head), k, ring);
             head >>= 8 * k;
-            // q = head / p, r = head % p (src/ans.rs:101-102)
-            uint64_t q = qest(head, e.rcp);
+            // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
+            // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q' in {q, q+1} and
+            // r' = head - q'*p in (-p, p): head = norm*q' + (cum + r' + [r' < 0]*(p - norm)),
+            // a signed 32-bit addend, so the q' - 1 fix-up never touches 64 bits.
+            const uint64_t q = qest(head, e.rcp);
             const int32_t rr = static_cast<int32_t>(lo32(head) - lo32(q) * e.mass);
-            const uint32_t neg = rr < 0 ? 1u : 0u;
-            q -= neg;
-            const uint32_t r = static_cast<uint32_t>(rr) + (neg ? e.mass : 0u);
-            // head = norm * q + cdf(x, r) (src/ans.rs:103-104, src/codec.rs:64)
-            head = q * norm + (static_cast<uint64_t>(e.cum) + r);
+            const int32_t adj = rr < 0 ? static_cast<int32_t>(e.mass - static_cast<uint32_t>(norm)) : 0;
+            const int32_t a = static_cast<int32_t>(e.cum) + rr + adj;
+            head = q * norm + static_cast<uint64_t>(static_cast<int64_t>(a));
         }
     };
 
