@@ -303,6 +303,18 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ 
     for (uint32_t k = lane; k < lens[c]; k += 64) d[k] = s[k];
 }
 
+// One wave per chunk copies a dense-container stream into its slot (the inverse of k_compact).
+__global__ __launch_bounds__(kBlock) void k_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offsets,
+                                                   const uint32_t* __restrict__ lens, uint64_t nchunks,
+                                                   uint8_t* __restrict__ slots, uint64_t slot_cap) {
+    const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
+    const uint8_t* s = in + offsets[c];
+    uint8_t* d = slots + c * slot_cap;
+    for (uint32_t k = lane; k < lens[c]; k += 64) d[k] = s[k];
+}
+
 // ------------------------------------------------------------------ launch helpers
 
 inline hipStream_t pick(ans_gpu_table* gt, void* stream) {
@@ -727,21 +739,33 @@ int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len,
         if (lens[j] > 0xffffffffull || offsets[j] > in_len || lens[j] > in_len - offsets[j]) return ANS_E_LEN;
         l32[j] = static_cast<uint32_t>(lens[j]);
     }
+    // The container is expanded into the encoder's slot layout on the device, so full chunks
+    // take the fast kernel; slots are widened if a (possibly corrupt) stream is longer than
+    // the worst case of a valid one.
+    uint64_t slot_cap = 0, max_len = 0;
+    ans_gpu_slot_capacity(gt, chunk_len, &slot_cap);
+    for (uint64_t j = 0; j < nchunks; ++j) max_len = std::max<uint64_t>(max_len, l32[j]);
+    slot_cap = std::max<uint64_t>(slot_cap, (max_len + 64 + 127) & ~uint64_t(127));
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = gt->g->stream;
-    DevBuf d_in, d_off, d_lens, d_status, d_out;
+    DevBuf d_in, d_off, d_lens, d_status, d_out, d_slots;
     HIP_TRY(d_in.alloc(in_len + 16));
     HIP_TRY(d_off.alloc(nchunks * sizeof(uint64_t)));
     HIP_TRY(d_lens.alloc(nchunks * sizeof(uint32_t)));
     HIP_TRY(d_status.alloc(sizeof(uint32_t)));
     HIP_TRY(d_out.alloc(n * sym_bytes));
+    HIP_TRY(d_slots.alloc(nchunks * slot_cap));
     if (in_len) HIP_TRY(hipMemcpyAsync(d_in.p, in, in_len, hipMemcpyHostToDevice, s));
     if (nchunks) {
         HIP_TRY(hipMemcpyAsync(d_off.p, offsets, nchunks * sizeof(uint64_t), hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_lens.p, l32.data(), nchunks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        k_expand<<<grid_for(nchunks * 64), kBlock, 0, s>>>(static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_off.p),
+                                                           static_cast<uint32_t*>(d_lens.p), nchunks,
+                                                           static_cast<uint8_t*>(d_slots.p), slot_cap);
+        HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMemsetAsync(d_status.p, 0, sizeof(uint32_t), s));
-    int rc = ans_dev_decode_chunks(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_off.p), 0,
+    int rc = ans_dev_decode_chunks(gt, static_cast<uint8_t*>(d_slots.p), nullptr, slot_cap,
                                    static_cast<uint32_t*>(d_lens.p), n, chunk_len, gen_kind, d_out.p, sym_bytes,
                                    static_cast<uint32_t*>(d_status.p), s);
     if (rc) return rc;

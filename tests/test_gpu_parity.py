@@ -225,3 +225,50 @@ def test_c4_shard_u16_round_trip(gpu):
     # SURVEY.md §8d C4 table (65,536 symbols, norm 134,561,356); one 2^27-symbol shard
     total = _device_roundtrip(gpu, A.c4_masses(), 1 << 27, 4096, 2, 2, 32)
     assert 1.9 < total / (1 << 27) < 2.1
+
+
+@pytest.mark.parametrize("sym_bytes", [1, 2])
+def test_dense_and_slot_layouts_decode_alike(gpu, sym_bytes):
+    """ans_dev_decode_chunks on the dense container (explicit offsets: generic kernel) and on
+    the encoder's slot layout (fast kernel) give the same symbols and status."""
+    torch = pytest.importorskip("torch")
+    dt = {1: torch.uint8, 2: torch.int16}[sym_bytes]
+    masses = A.c3_masses()
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    try:
+        n, L = 700 * 4096 + 333, 4096
+        nchunks = -(-n // L)
+        cap = gt.slot_capacity(L)
+        syms = torch.empty(n, dtype=dt, device="cuda")
+        gt.dev_gen_iid(9, 0, n, syms, sym_bytes, stream)
+        slots = torch.empty(nchunks * cap, dtype=torch.uint8, device="cuda")
+        lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        gt.dev_encode(syms, sym_bytes, n, L, slots, cap, lens, status, stream)
+        offsets = torch.zeros(nchunks, dtype=torch.int64, device="cuda")
+        offsets[1:] = torch.cumsum(lens.to(torch.int64), 0)[:-1]
+        dense = torch.empty(int(lens.to(torch.int64).sum().item()) + 16, dtype=torch.uint8, device="cuda")
+        gpu.compact(slots, cap, lens, offsets, nchunks, dense, stream)
+        out_fast = torch.empty_like(syms)
+        out_generic = torch.empty_like(syms)
+        gt.dev_decode(slots, None, cap, lens, n, L, out_fast, sym_bytes, status, stream)
+        gt.dev_decode(dense, offsets, 0, lens, n, L, out_generic, sym_bytes, status, stream)
+        assert gpu.status(status, stream) == 0
+        assert torch.equal(out_fast, syms) and torch.equal(out_generic, syms)
+        # a corrupted stream is caught by both layouts
+        j = 123
+        slots[j * cap + 5] ^= 0x5A
+        dense[int(offsets[j].item()) + 5] ^= 0x5A
+        status.zero_()
+        gt.dev_decode(slots, None, cap, lens, n, L, out_fast, sym_bytes, status, stream)
+        st_fast = gpu.status(status, stream)
+        status.zero_()
+        gt.dev_decode(dense, offsets, 0, lens, n, L, out_generic, sym_bytes, status, stream)
+        st_generic = gpu.status(status, stream)
+        assert st_fast == st_generic == A.ANS_E_MISMATCH
+        assert torch.equal(out_fast, out_generic)
+    finally:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(torch.cuda.default_stream())
