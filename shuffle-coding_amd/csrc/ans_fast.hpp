@@ -31,6 +31,8 @@ namespace fast {
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
+constexpr uint32_t kEncMcOffset = 8 * 257;  // encode LDS: rcp[257] then (mass, cum)[257]
+constexpr uint32_t kEncLdsBytes = 2 * kEncMcOffset;
 constexpr uint32_t kDecTableBytes = 14336;  // decode buckets in LDS: 2 x (66 KiB ring + 14 KiB) per CU
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
@@ -115,13 +117,31 @@ __device__ __forceinline__ void flush_page(const Ring& ring, uint32_t p, uint8_t
 }
 
 // KMAX: most bytes one push can emit (table property); kK32: K < 2^32 (norm > 2^24).
-template <typename Sym, int KMAX, bool kK32>
-__global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
-                                                      uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
-                                                      uint32_t* __restrict__ lens, uint32_t* __restrict__ status) {
+// kGlobalRows: the rows stay in global memory (alphabets above 256 symbols, e.g. C4's 65,536:
+// 1 MiB of rows, L2-resident); each unit's rows are then requested at the point BEFORE the
+// unit that uses them, so their latency hides behind one unit of work.
+template <typename Sym, int KMAX, bool kK32, bool kGlobalRows>
+__global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTable t, const Sym* __restrict__ syms,
+                                                                         uint64_t chunk_len, uint64_t nfull,
+                                                                         uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                                         uint32_t* __restrict__ lens,
+                                                                         uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
-    EncRow* rows = reinterpret_cast<EncRow*>(lds);
-    for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) rows[i] = t.enc[i];
+    // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
+    // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
+    double* rcps = reinterpret_cast<double*>(lds);
+    uint2* mcs = reinterpret_cast<uint2*>(lds + kEncMcOffset);  // fixed offset: immediate ds offsets
+    if (!kGlobalRows) {
+        for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) {
+            const EncRow r = t.enc[i];
+            rcps[i] = r.rcp;
+            mcs[i] = make_uint2(r.mass, r.cum);
+        }
+    }
+    auto row = [&](uint32_t s) __attribute__((always_inline)) {
+        const uint2 mc = mcs[s];
+        return EncRow{rcps[s], mc.x, mc.y};
+    };
     const Ring ring{reinterpret_cast<uint32_t*>(lds + t.enc_lds_bytes) + threadIdx.x};
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -151,35 +171,46 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
             ++fp;
         }
     };
+    auto push_one = [&](const EncRow& e) __attribute__((always_inline)) {
+        asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
+        // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
+        const uint64_t pK = kK32 ? static_cast<uint64_t>(e.mass) * static_cast<uint32_t>(K)
+                                 : static_cast<uint64_t>(e.mass) * K;
+        uint32_t k = (head >> 8) >= pK ? 1u : 0u;
+        if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 1u : 0u;
+        if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 1u : 0u;
+        if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
+        f.push<KMAX>(lo32(head), k, ring);
+        head >>= 8 * k;
+        // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
+        // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q' in {q, q+1} and
+        // r' = head - q'*p in (-p, p): head = norm*q' + (cum + r' + [r' < 0]*(p - norm)),
+        // a signed 32-bit addend, so the q' - 1 fix-up never touches 64 bits.
+        const uint64_t q = qest(head, e.rcp);
+        const int32_t rr = static_cast<int32_t>(lo32(head) - lo32(q) * e.mass);
+        const int32_t adj = rr < 0 ? static_cast<int32_t>(e.mass - static_cast<uint32_t>(norm)) : 0;
+        const int32_t a = static_cast<int32_t>(e.cum) + rr + adj;
+        head = q * norm + static_cast<uint64_t>(static_cast<int64_t>(a));
+    };
     auto process = [&](const uint4& unit) __attribute__((always_inline)) {
         // rows are read one symbol ahead; the scheduling barriers keep the compiler from
         // hoisting all sixteen reads (and their registers) to the top of the unit
-        EncRow e_next = rows[min(sym_of<Sym>(unit, U - 1), sentinel)];
+        EncRow e_next = row(min(sym_of<Sym>(unit, U - 1), sentinel));
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             __builtin_amdgcn_sched_barrier(0);
             const EncRow e = e_next;
-            if (j > 0) e_next = rows[min(sym_of<Sym>(unit, j - 1), sentinel)];
-            asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
-            // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
-            const uint64_t pK = kK32 ? static_cast<uint64_t>(e.mass) * static_cast<uint32_t>(K)
-                                     : static_cast<uint64_t>(e.mass) * K;
-            uint32_t k = (head >> 8) >= pK ? 1u : 0u;
-            if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 1u : 0u;
-            if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 1u : 0u;
-            if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
-            f.push<KMAX>(lo32(head), k, ring);
-            head >>= 8 * k;
-            // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
-            // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q' in {q, q+1} and
-            // r' = head - q'*p in (-p, p): head = norm*q' + (cum + r' + [r' < 0]*(p - norm)),
-            // a signed 32-bit addend, so the q' - 1 fix-up never touches 64 bits.
-            const uint64_t q = qest(head, e.rcp);
-            const int32_t rr = static_cast<int32_t>(lo32(head) - lo32(q) * e.mass);
-            const int32_t adj = rr < 0 ? static_cast<int32_t>(e.mass - static_cast<uint32_t>(norm)) : 0;
-            const int32_t a = static_cast<int32_t>(e.cum) + rr + adj;
-            head = q * norm + static_cast<uint64_t>(static_cast<int64_t>(a));
+            if (j > 0) e_next = row(min(sym_of<Sym>(unit, j - 1), sentinel));
+            push_one(e);
         }
+    };
+    auto request_rows = [&](const uint4& unit, EncRow* buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) buf[j] = t.enc[min(sym_of<Sym>(unit, j), sentinel)];
+    };
+    auto process_rows = [&](const EncRow* buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = U - 1; j >= 0; --j) push_one(buf[j]);
     };
 
     // groups are walked last to first; group g-1's 64 bytes are requested while g is coded
@@ -191,23 +222,51 @@ __global__ __launch_bounds__(kBlock, 4) void k_encode(FastTable t, const Sym* __
         n2 = gsrc[2];
         n3 = gsrc[3];
     }
-    for (int g = ngroups - 1; g >= 0; --g) {
-        point();
-        const uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
-        {
-            const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
-            n0 = gsrc[0];
-            n1 = gsrc[1];
-            n2 = gsrc[2];
-            n3 = gsrc[3];
+    if constexpr (kGlobalRows) {
+        EncRow ra[U], rb[U];
+        wait_vm();
+        request_rows(n3, ra);
+        for (int g = ngroups - 1; g >= 0; --g) {
+            point();
+            const uint4 c0 = n0, c1 = n1, c2 = n2;
+            {
+                const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
+                n0 = gsrc[0];
+                n1 = gsrc[1];
+                n2 = gsrc[2];
+                n3 = gsrc[3];
+            }
+            request_rows(c2, rb);
+            process_rows(ra);  // unit 3 of group g
+            point();
+            request_rows(c1, ra);
+            process_rows(rb);
+            point();
+            request_rows(c0, rb);
+            process_rows(ra);
+            point();
+            request_rows(n3, ra);  // unit 3 of group g-1 (landed at the previous point)
+            process_rows(rb);
         }
-        process(c3);
-        point();
-        process(c2);
-        point();
-        process(c1);
-        point();
-        process(c0);
+    } else {
+        for (int g = ngroups - 1; g >= 0; --g) {
+            point();
+            const uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+            {
+                const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
+                n0 = gsrc[0];
+                n1 = gsrc[1];
+                n2 = gsrc[2];
+                n3 = gsrc[3];
+            }
+            process(c3);
+            point();
+            process(c2);
+            point();
+            process(c1);
+            point();
+            process(c0);
+        }
     }
     wait_vm();
 

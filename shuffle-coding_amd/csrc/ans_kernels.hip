@@ -327,9 +327,9 @@ inline unsigned grid_for(uint64_t lanes) { return static_cast<unsigned>((lanes +
 // allows it; everything else (ragged last chunk, odd chunk lengths, other tables) to the
 // generic kernel.  Both write the same slot layout and identical bytes.
 template <typename Sym>
-uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len) {
+uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len, bool decode) {
     if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % fast::kGroupBytes != 0) return 0;
-    if (sizeof(Sym) == 1 && gt->ft.nsym > 256) return 0;
+    if (decode ? !gt->ft.dec_usable : (sizeof(Sym) == 1 && gt->ft.enc_global)) return 0;
     return n / chunk_len;
 }
 
@@ -340,19 +340,30 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     const Sym* syms = static_cast<const Sym*>(d_syms);
-    const uint64_t nfull = fast_chunks<Sym>(gt, n, chunk_len);
+    const uint64_t nfull = fast_chunks<Sym>(gt, n, chunk_len, false);
     if (nfull) {
         const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         const size_t lds = ft.enc_lds_bytes + sizeof(uint32_t) * fast::kRingDwords * fast::kBlock;
-#define ENC(KM, K32) fast::k_encode<Sym, KM, K32><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
         const bool k32 = ft.K < (1ull << 32);
-        switch (ft.kmax) {
-        case 1:
-        case 2: if (k32) ENC(2, true); else ENC(2, false); break;
-        case 3: if (k32) ENC(3, true); else ENC(3, false); break;
-        default: if (k32) ENC(4, true); else ENC(4, false); break;
+#define ENC(KM, K32, G) fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
+#define ENC_KMAX(G)                                                   \
+        switch (ft.kmax) {                                            \
+        case 1:                                                       \
+        case 2: if (k32) ENC(2, true, G); else ENC(2, false, G); break; \
+        case 3: if (k32) ENC(3, true, G); else ENC(3, false, G); break; \
+        default: if (k32) ENC(4, true, G); else ENC(4, false, G); break; \
         }
+        if constexpr (sizeof(Sym) > 1) {
+            if (ft.enc_global) {
+                ENC_KMAX(true)
+            } else {
+                ENC_KMAX(false)
+            }
+        } else {
+            ENC_KMAX(false)
+        }
+#undef ENC_KMAX
 #undef ENC
         HIP_TRY(hipGetLastError());
     }
@@ -380,7 +391,7 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const DevTable& t = gt->t;
     Sym* out = static_cast<Sym*>(d_syms);
     // the fast kernel reads the encoder's 64-byte-aligned slot layout only
-    const uint64_t nfull = (d_offsets == nullptr && slot_cap % 64 == 0) ? fast_chunks<Sym>(gt, n, chunk_len) : 0;
+    const uint64_t nfull = (d_offsets == nullptr && slot_cap % 64 == 0) ? fast_chunks<Sym>(gt, n, chunk_len, true) : 0;
     if (nfull) {
         const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
@@ -436,12 +447,13 @@ struct DevBuf {
 };
 
 // Derives the fast-path tables (ans_table.hpp FastTable) when the table qualifies:
-// 2^16 <= norm <= 2^31 (f64 quotient estimate) and nsym <= 256 (LDS-resident
-// rows and 8-bit icdf buckets).
+// 2^16 <= norm <= 2^31 (f64 quotient estimate) and nsym <= 65536.  Up to 256
+// symbols the rows and decode buckets are staged in LDS; above, the encoder reads its rows
+// from global memory and decoding uses the generic kernel.
 int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const DevTable& t = gt->t;
     FastTable ft{};
-    if (!t.fast || t.nsym > 256) {
+    if (!t.fast || t.nsym > 65536) {
         gt->ft = ft;
         return ANS_OK;
     }
@@ -458,11 +470,14 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         for (uint32_t j = 1; j <= 4; ++j)  // can a push emit j bytes? (head < 2^64 <= p*K*2^8j otherwise)
             if ((pK << (8 * j)) < (static_cast<u128>(1) << 64) && j > kmax) kmax = j;
     }
-    // decode buckets: the finest power-of-two width whose table fits fast::kDecTableBytes
+    ft.enc_global = nsym > 256;
+    ft.dec_usable = nsym <= 256;
+    // decode buckets: the finest power-of-two width whose table fits fast::kDecTableBytes in
+    // LDS (with the cdf table); for large alphabets, at most 2^16 buckets in global memory
     uint32_t shift = 0;
     const size_t cum_bytes = sizeof(uint32_t) * (nsym + 5);
-    while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > (fast::kDecTableBytes - cum_bytes) / sizeof(DecBucket))
-        ++shift;
+    const uint64_t max_buckets = ft.dec_usable ? (fast::kDecTableBytes - cum_bytes) / sizeof(DecBucket) : (1u << 16);
+    while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > max_buckets) ++shift;
     const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1);
     std::vector<uint32_t> cum(nsym + 5, t.norm);
     for (uint32_t s = 0; s < nsym; ++s) cum[s] = static_cast<uint32_t>(cat.cummasses[s]);
@@ -478,7 +493,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_buckets = nb;
     ft.dec_shift = shift;
     ft.norm = t.norm;
-    ft.enc_lds_bytes = static_cast<uint32_t>((sizeof(EncRow) * enc.size() + 15) & ~size_t(15));
+    ft.enc_lds_bytes = fast::kEncLdsBytes;  // nsym + 1 <= 257 rows, split (ans_fast.hpp)
     ft.dec_cum_off = static_cast<uint32_t>((sizeof(DecBucket) * dec.size() + 15) & ~size_t(15));
     ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;

@@ -74,7 +74,9 @@ struct FastTable {
     uint64_t K;
     uint64_t L;
     double rcp_norm;
-    uint32_t usable;
+    uint32_t usable;      // encode fast path available (2^16 <= norm <= 2^31)
+    uint32_t enc_global;  // rows read from global memory (nsym > 256; ans_fast.hpp kGlobalRows)
+    uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
 };
 
 }  // namespace shuffle_coding
