@@ -36,6 +36,16 @@ constexpr uint32_t kEncLdsBytes = 2 * kEncMcOffset;
 constexpr uint32_t kDecTableBytes = 14336;  // decode buckets in LDS: 2 x (66 KiB ring + 14 KiB) per CU
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
+// Non-temporal 16-byte global load / store (streamed data that must not evict cached tables).
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load(const uint4* p) {
+    const v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
+    __builtin_nontemporal_store(v4u32{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u32*>(p));
+}
+
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
@@ -107,13 +117,18 @@ struct Funnel {
     }
 };
 
+template <bool kNT = false>
 __device__ __forceinline__ void flush_page(const Ring& ring, uint32_t p, uint8_t* dst) {
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = ring.at(static_cast<int32_t>(16 * p + i));
     uint4* d = reinterpret_cast<uint4*>(dst + 64ull * p);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        if (kNT) nt_store(d + q, v);
+        else d[q] = v;
+    }
 }
 
 // KMAX: most bytes one push can emit (table property); kK32: K < 2^32 (norm > 2^24).
@@ -166,7 +181,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto point = [&]() __attribute__((always_inline)) {
         wait_vm();
         if ((f.wd >> 4) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
-            if (fp < npages_cap) flush_page(ring, fp, dst);
+            if (fp < npages_cap) flush_page<kGlobalRows>(ring, fp, dst);
             else over = 1;
             ++fp;
         }
@@ -213,14 +228,17 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         for (int j = U - 1; j >= 0; --j) push_one(buf[j]);
     };
 
+    // symbols are streamed once: with rows in global memory they go non-temporal so that they
+    // do not evict the rows from L2
+    auto load_sym = [&](const uint4* p) __attribute__((always_inline)) { return kGlobalRows ? nt_load(p) : *p; };
     // groups are walked last to first; group g-1's 64 bytes are requested while g is coded
     uint4 n0, n1, n2, n3;
     {
         const uint4* gsrc = src + 4 * (ngroups - 1);
-        n0 = gsrc[0];
-        n1 = gsrc[1];
-        n2 = gsrc[2];
-        n3 = gsrc[3];
+        n0 = load_sym(gsrc + 0);
+        n1 = load_sym(gsrc + 1);
+        n2 = load_sym(gsrc + 2);
+        n3 = load_sym(gsrc + 3);
     }
     if constexpr (kGlobalRows) {
         EncRow ra[U], rb[U];
@@ -231,10 +249,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             const uint4 c0 = n0, c1 = n1, c2 = n2;
             {
                 const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
-                n0 = gsrc[0];
-                n1 = gsrc[1];
-                n2 = gsrc[2];
-                n3 = gsrc[3];
+                n0 = load_sym(gsrc + 0);
+                n1 = load_sym(gsrc + 1);
+                n2 = load_sym(gsrc + 2);
+                n3 = load_sym(gsrc + 3);
             }
             request_rows(c2, rb);
             process_rows(ra);  // unit 3 of group g
@@ -254,10 +272,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             const uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
             {
                 const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
-                n0 = gsrc[0];
-                n1 = gsrc[1];
-                n2 = gsrc[2];
-                n3 = gsrc[3];
+                n0 = load_sym(gsrc + 0);
+                n1 = load_sym(gsrc + 1);
+                n2 = load_sym(gsrc + 2);
+                n3 = load_sym(gsrc + 3);
             }
             process(c3);
             point();
@@ -278,7 +296,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     if (f.n) ring.at(static_cast<int32_t>(f.wd)) = f.a1 >> (8 * (4 - f.n));
     const uint32_t len = 4 * f.wd + f.n;
     for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
-        if (fp < npages_cap) flush_page(ring, fp, dst);
+        if (fp < npages_cap) flush_page<kGlobalRows>(ring, fp, dst);
         else over = 1;
     }
     if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
@@ -502,6 +520,210 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
     const int32_t remaining = ch.P + 4;  // < 0: generated
+    if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
+    else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+}
+
+// ====================================================================== decode, large alphabets
+// Alphabets above 256 symbols (C4: 65,536) keep their decode buckets in global memory
+// (DecBucketG, 32 B: cdf(s0..s0+5) and s0, at most 2^16 buckets = 2 MiB, L2-resident): one load
+// per symbol on the dependency chain.  gfx9 retires vector-memory operations in issue order, so
+// every such load also waits for the ring's page fetches and the symbol stores issued before
+// it; those are therefore batched per BLOCK (four units = 64 bytes of symbols per lane) and
+// issued together at the block's point, which exposes one HBM latency per block instead of
+// one per unit.  The ring has four pages (65 rows, row 64 mirrors row 0); a block pops at most
+// 4U*KMAX <= 128 bytes, and up to two pages land per point, so reads never reach an unlanded
+// page.
+constexpr int kDecGRows = 65;
+constexpr uint32_t kDecGRingBytes = kDecGRows * kBlock * 4;
+
+struct DecChainG {
+    uint32_t* ring;  // &ring[0][lane]
+    const uint8_t* src;
+    uint4 S0[4], S1[4];  // pages low-1 and low-2, in flight
+    int32_t low, P;
+    uint32_t wx, wy, W;
+    uint64_t head;
+    uint64_t qq;
+    uint32_t cf, cum, nxt, sx;
+    bool far;
+
+    __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kBlock]; }
+    __device__ __forceinline__ void put_page(int32_t p, const uint4* S) {
+        const int32_t r0 = (p & 3) * 16;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            row(r0 + 4 * k + 0) = S[k].x;
+            row(r0 + 4 * k + 1) = S[k].y;
+            row(r0 + 4 * k + 2) = S[k].z;
+            row(r0 + 4 * k + 3) = S[k].w;
+        }
+        if ((p & 3) == 0) row(64) = S[0].x;
+    }
+    __device__ __forceinline__ void fetch_page(int32_t p, uint4* S) {
+        if (p >= 0) {
+            // streamed once: non-temporal, so the pages do not evict the bucket table from L2
+            const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S[k] = nt_load(g + k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S[k] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void read_window() {
+        const uint32_t* a = ring + ((static_cast<uint32_t>(P) >> 2) & 63u) * kBlock;
+        wy = a[0];
+        wx = a[kBlock];
+    }
+    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P) & 3u); }
+    // the top four pages land before decoding starts; the next two are requested
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
+        src = s;
+        const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
+        fetch_page(len > 0 ? top : -1, S0);
+        fetch_page(top - 1, S1);
+        wait_vm();
+        put_page(top, S0);
+        put_page(top - 1, S1);
+        fetch_page(top - 2, S0);
+        fetch_page(top - 3, S1);
+        wait_vm();
+        put_page(top - 2, S0);
+        put_page(top - 3, S1);
+        low = top - 3;
+        fetch_page(low - 1, S0);
+        fetch_page(low - 2, S1);
+        P = len - 4;
+        read_window();
+        head = 0;
+    }
+    __device__ __forceinline__ void pull_until(uint64_t bound) {
+        for (int g = 0; g < 9 && head < bound; ++g) {
+            form_window();
+            head = (head << 8) | (W >> 24);
+            P -= 1;
+            read_window();
+        }
+    }
+    // at a block point, after s_waitcnt vmcnt(0): land what the read frontier allows
+    __device__ __forceinline__ void point() {
+        const int32_t f = ((P >> 2) + 1) >> 4;  // page of the highest dword still to be read
+        const bool l1 = f <= low + 2;           // page low-1 may take page low+3's slot
+        const bool l2 = f <= low + 1;           // page low-2 may take page low+2's slot
+        if (l1) put_page(low - 1, S0);
+        if (l2) {
+            put_page(low - 2, S1);
+            low -= 2;
+            fetch_page(low - 1, S0);
+            fetch_page(low - 2, S1);
+        } else if (l1) {
+            low -= 1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S0[k] = S1[k];
+            fetch_page(low - 2, S1);
+        }
+    }
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
+        form_window();
+        const uint32_t h1 = hi32(head), h0 = lo32(head);
+        const uint32_t js = static_cast<uint32_t>(__builtin_clzll(head | 1)) >> 3;
+        const uint32_t sh = 4u - js;
+        const uint32_t xj1 = ab(h1, h0, sh), xj0 = ab(h0, W, sh);
+        const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
+        const bool one_less = mk64(xm1, xm0) >= L;
+        const bool keep = h1 >= (1u << 24);
+        const uint32_t k = keep ? 0u : js - (one_less ? 1u : 0u);
+        head = keep ? head : (one_less ? mk64(xm1, xm0) : mk64(xj1, xj0));
+        P -= static_cast<int32_t>(k);
+        read_window();
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t q = qest(head, rcp_norm);
+        const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
+        const uint32_t neg = ii < 0 ? 1u : 0u;
+        qq = q - neg;
+        cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
+    }
+    __device__ __forceinline__ void lookup(const DecBucketG* __restrict__ bkt, uint32_t shift) {
+        const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
+        uint4 a = e[0], b = e[1];  // c0..c3 | c4, c5, s0, -
+        // both loads complete here (no loads sunk into the selects' branches)
+        asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z));
+        const bool b1 = cf >= a.y, b2 = cf >= a.z, b3 = cf >= a.w, b4 = cf >= b.x;
+        cum = b4 ? b.x : (b3 ? a.w : (b2 ? a.z : (b1 ? a.y : a.x)));
+        nxt = b4 ? b.y : (b3 ? b.x : (b2 ? a.w : (b1 ? a.z : a.y)));
+        sx = b.z + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
+        far = cf >= b.y;
+    }
+    __device__ __forceinline__ void lookup_far(const uint32_t* __restrict__ gcum) {
+        if (far) {
+            sx += 1;
+            while (cf >= gcum[sx + 1]) ++sx;
+            cum = gcum[sx];
+            nxt = gcum[sx + 1];
+        }
+    }
+    __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
+};
+
+template <typename Sym>
+__global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8_t* __restrict__ slots,
+                                                        uint64_t slot_cap, const uint32_t* __restrict__ lens,
+                                                        uint64_t chunk_len, uint64_t nfull, int gen_kind,
+                                                        Sym* __restrict__ out, uint32_t* __restrict__ status) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= nfull) return;  // no barrier below: lanes are independent
+
+    constexpr int U = 16 / static_cast<int>(sizeof(Sym));
+    static_assert(U * 4 * 4 <= 128, "a block pops at most two pages");
+    const int nblocks = static_cast<int>(chunk_len / (4 * U));
+    const uint64_t L = t.L;
+    const uint32_t norm = t.norm;
+    const double rcp_norm = t.rcp_norm;
+    const uint32_t shift = t.dec_shift;
+    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
+
+    DecChainG ch;
+    ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
+    ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
+    ch.pull_until(L);
+
+    uint4 q[4];
+    for (int b = 0; b < nblocks; ++b) {
+        wait_vm();  // block point
+        if (b > 0) {
+            uint4* d = dst + 4 * (b - 1);
+            nt_store(d + 0, q[0]);
+            nt_store(d + 1, q[1]);
+            nt_store(d + 2, q[2]);
+            nt_store(d + 3, q[3]);
+        }
+        ch.point();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint4 outv = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                ch.renorm_div(L, norm, rcp_norm);
+                ch.lookup(t.dbkt_g, shift);
+                if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(t.cum);
+                ch.update();
+                put_sym<Sym>(outv, j, ch.sx);
+            }
+            q[u] = outv;
+        }
+    }
+    wait_vm();
+    if (nblocks > 0) {
+        uint4* d = dst + 4 * (nblocks - 1);
+        d[0] = q[0];
+        d[1] = q[1];
+        d[2] = q[2];
+        d[3] = q[3];
+    }
+    ch.pull_until(kMaxMinHead);
+    const int32_t remaining = ch.P + 4;
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }

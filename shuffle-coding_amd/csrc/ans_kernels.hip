@@ -389,18 +389,27 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
+    const FastTable& ft = gt->ft;
     Sym* out = static_cast<Sym*>(d_syms);
-    // the fast kernel reads the encoder's 64-byte-aligned slot layout only
-    const uint64_t nfull = (d_offsets == nullptr && slot_cap % 64 == 0) ? fast_chunks<Sym>(gt, n, chunk_len, true) : 0;
+    // the fast kernels read the encoder's 64-byte-aligned slot layout only
+    const bool slots = d_offsets == nullptr && slot_cap % 64 == 0;
+    const bool lds_table = slots && fast_chunks<Sym>(gt, n, chunk_len, true) > 0;
+    const bool global_table = slots && sizeof(Sym) > 1 && ft.usable && ft.dec_global &&
+                              (chunk_len * sizeof(Sym)) % fast::kGroupBytes == 0;
+    const uint64_t nfull = (lds_table || global_table) ? n / chunk_len : 0;
     if (nfull) {
-        const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
-        const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
         constexpr int U = 16 / sizeof(Sym);
-        if (U * ft.kmax > 60)
-            fast::k_decode<Sym, U / 2><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
-        else
-            fast::k_decode<Sym, U><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+        if (global_table) {
+            if constexpr (sizeof(Sym) > 1)
+                fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+        } else {
+            const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
+            if (U * ft.kmax > 60)
+                fast::k_decode<Sym, U / 2><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+            else
+                fast::k_decode<Sym, U><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+        }
         HIP_TRY(hipGetLastError());
     }
     if (nfull == nchunks) return ANS_OK;
@@ -476,18 +485,31 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     // LDS (with the cdf table); for large alphabets, at most 2^16 buckets in global memory
     uint32_t shift = 0;
     const size_t cum_bytes = sizeof(uint32_t) * (nsym + 5);
-    const uint64_t max_buckets = ft.dec_usable ? (fast::kDecTableBytes - cum_bytes) / sizeof(DecBucket) : (1u << 16);
+    static const uint32_t g_bits = [] {  // experiment knob: global bucket table size
+        const char* e = getenv("ANS_DECG_BUCKET_BITS");
+        return e ? static_cast<uint32_t>(atoi(e)) : 16u;
+    }();
+    const uint64_t max_buckets = ft.dec_usable ? (fast::kDecTableBytes - cum_bytes) / sizeof(DecBucket) : (1ull << g_bits);
     while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > max_buckets) ++shift;
     const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1);
-    std::vector<uint32_t> cum(nsym + 5, t.norm);
+    std::vector<uint32_t> cum(nsym + 6, t.norm);
     for (uint32_t s = 0; s < nsym; ++s) cum[s] = static_cast<uint32_t>(cat.cummasses[s]);
-    std::vector<DecBucket> dec(nb);
+    std::vector<DecBucket> dec(ft.dec_usable ? nb : 0);
+    std::vector<DecBucketG> decg(ft.dec_usable ? 0 : nb);
     for (uint32_t j = 0; j < nb; ++j) {
         const uint32_t s0 = static_cast<uint32_t>(cat.icdf(static_cast<uint64_t>(j) << shift).first);
-        DecBucket& d = dec[j];
-        for (int i = 0; i < 5; ++i) d.c[i] = cum[s0 + i];
-        d.s0 = s0;
+        if (ft.dec_usable) {
+            DecBucket& d = dec[j];
+            for (int i = 0; i < 5; ++i) d.c[i] = cum[s0 + i];
+            d.s0 = s0;
+        } else {
+            DecBucketG& d = decg[j];
+            for (int i = 0; i < 6; ++i) d.c[i] = cum[s0 + i];
+            d.s0 = s0;
+            d.pad = 0;
+        }
     }
+    ft.dec_global = !ft.dec_usable;
     ft.nsym = nsym;
     ft.enc_rows = nsym + 1;
     ft.dec_buckets = nb;
@@ -501,15 +523,19 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.L = t.L;
     ft.rcp_norm = t.rcp_norm;
     const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = sizeof(DecBucket) * dec.size();
+    const size_t decg_b = sizeof(DecBucketG) * decg.size();
     const size_t o_dec = (enc_b + 255) & ~size_t(255), o_cum = o_dec + ((dec_b + 255) & ~size_t(255));
+    const size_t o_decg = o_cum + ((sizeof(uint32_t) * cum.size() + 255) & ~size_t(255));
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
-    HIP_TRY(hipMalloc(&mem, o_cum + sizeof(uint32_t) * cum.size()));
+    HIP_TRY(hipMalloc(&mem, o_decg + decg_b));
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_dec, dec.data(), dec_b, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_cum, cum.data(), sizeof(uint32_t) * cum.size(), hipMemcpyHostToDevice));
+    if (decg_b) HIP_TRY(hipMemcpy(base + o_decg, decg.data(), decg_b, hipMemcpyHostToDevice));
+    ft.dbkt_g = reinterpret_cast<const DecBucketG*>(base + o_decg);
     ft.enc = reinterpret_cast<const EncRow*>(base);
     ft.dbkt = reinterpret_cast<const DecBucket*>(base + o_dec);
     ft.cum = reinterpret_cast<const uint32_t*>(base + o_cum);

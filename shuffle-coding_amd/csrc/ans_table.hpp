@@ -58,10 +58,18 @@ struct alignas(8) DecBucket {
     uint32_t c[5];
     uint32_t s0;
 };
+// Decode bucket for large alphabets (32 B, two 16-B global loads): cdf(s0..s0+5) and s0, so
+// five candidates per bucket.
+struct alignas(16) DecBucketG {
+    uint32_t c[6];
+    uint32_t s0;
+    uint32_t pad;
+};
 struct FastTable {
     const EncRow* enc;        // enc_rows = nsym + 1 rows (last = zero-mass sentinel)
     const DecBucket* dbkt;    // dec_buckets entries
-    const uint32_t* cum;      // cdf(s) for s = 0..nsym+4 (norm from nsym on): the slow icdf path
+    const uint32_t* cum;      // cdf(s) for s = 0..nsym+5 (norm from nsym on): the slow icdf path
+    const DecBucketG* dbkt_g; // large alphabets: dec_buckets entries in global memory
     uint32_t nsym;
     uint32_t enc_rows;
     uint32_t dec_buckets;
@@ -77,6 +85,7 @@ struct FastTable {
     uint32_t usable;      // encode fast path available (2^16 <= norm <= 2^31)
     uint32_t enc_global;  // rows read from global memory (nsym > 256; ans_fast.hpp kGlobalRows)
     uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
+    uint32_t dec_global;  // decode fast path for nsym > 256 (k_decode_g, buckets in global memory)
 };
 
 }  // namespace shuffle_coding
