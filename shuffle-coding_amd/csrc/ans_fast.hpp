@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto point = [&]() __attribute__((always_inline)) {
         wait_vm();
         if ((f.wd >> 4) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
-            if (fp < npages_cap) flush_page<kGlobalRows>(ring, fp, dst);
+            if (fp < npages_cap) flush_page(ring, fp, dst);
             else over = 1;
             ++fp;
         }
@@ -228,9 +228,8 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         for (int j = U - 1; j >= 0; --j) push_one(buf[j]);
     };
 
-    // symbols are streamed once: with rows in global memory they go non-temporal so that they
-    // do not evict the rows from L2
-    auto load_sym = [&](const uint4* p) __attribute__((always_inline)) { return kGlobalRows ? nt_load(p) : *p; };
+    // (non-temporal symbol loads / page stores measured 28% SLOWER with rows in global memory)
+    auto load_sym = [&](const uint4* p) __attribute__((always_inline)) { return *p; };
     // groups are walked last to first; group g-1's 64 bytes are requested while g is coded
     uint4 n0, n1, n2, n3;
     {
@@ -296,7 +295,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     if (f.n) ring.at(static_cast<int32_t>(f.wd)) = f.a1 >> (8 * (4 - f.n));
     const uint32_t len = 4 * f.wd + f.n;
     for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
-        if (fp < npages_cap) flush_page<kGlobalRows>(ring, fp, dst);
+        if (fp < npages_cap) flush_page(ring, fp, dst);
         else over = 1;
     }
     if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
@@ -307,6 +306,34 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     }
     if (over) atomicOr(status, 1u << ANS_E_LEN);
     lens[c] = len;
+}
+
+// ---- shared decode steps
+// renorm_up (src/ans.rs:239-243) with W = the next four stream bytes (first byte on top):
+// head = head << 8k | the top k bytes of W, for the least k that makes head >= L; returns k.
+// With js = min(clz64(head) >> 3, 4), X = (h:W) >> (32 - 8js) is >= 2^56 >= L (or head itself
+// when js = 0), and k = js - 1 suffices iff X >> 8 is >= L already.  The head is >= K >= 2^25
+// after any pop in the fast range, so a zero high word means js = 4 (v_ffbh_u32(0) = ~0
+// saturates through the min).  X comes from byte permutes, exact for every js in 0..4.
+__device__ __forceinline__ uint32_t renorm_up(uint64_t& head, uint32_t W, uint64_t L) {
+    const uint32_t h1 = hi32(head), h0 = lo32(head);
+    uint32_t fb;
+    asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
+    const uint32_t js = min(fb >> 3, 4u);
+    const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(js, js, 0u);
+    const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
+    const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
+    const bool one_less = js != 0 && mk64(xm1, xm0) >= L;
+    head = one_less ? mk64(xm1, xm0) : mk64(xj1, xj0);
+    return js - (one_less ? 1u : 0u);
+}
+// q = head / norm, cf = head % norm (src/ans.rs:110-111): estimate, then one fix-up
+__device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rcp_norm, uint64_t& qq, uint32_t& cf) {
+    const uint64_t q = qest(head, rcp_norm);
+    const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
+    const uint32_t neg = ii < 0 ? 1u : 0u;
+    qq = q - neg;
+    cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
 }
 
 // ====================================================================== decode
@@ -397,27 +424,11 @@ struct DecChain {
     }
     // phase 1: renorm_up, q/cf, next window
     __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
-        // renorm_up (src/ans.rs:239-243) pulls k bytes: with js = clz(head) >> 3, (h:W) >> (32-8js)
-        // is >= 2^56 >= L, and k = js - 1 suffices iff that value >> 8 is >= L already.
         form_window();
-        const uint32_t h1 = hi32(head), h0 = lo32(head);
-        const uint32_t js = static_cast<uint32_t>(__builtin_clzll(head | 1)) >> 3;
-        const uint32_t sh = 4u - js;  // js in 1..4 here; js = 0 (head >= 2^56) is kept below
-        const uint32_t xj1 = ab(h1, h0, sh), xj0 = ab(h0, W, sh);
-        const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
-        const bool one_less = mk64(xm1, xm0) >= L;
-        const bool keep = h1 >= (1u << 24);
-        const uint32_t k = keep ? 0u : js - (one_less ? 1u : 0u);
-        head = keep ? head : (one_less ? mk64(xm1, xm0) : mk64(xj1, xj0));
-        P -= static_cast<int32_t>(k);
+        P -= static_cast<int32_t>(renorm_up(head, W, L));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        // q = head / norm, cf = head % norm (src/ans.rs:110-111)
-        uint64_t q = qest(head, rcp_norm);
-        const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
-        const uint32_t neg = ii < 0 ? 1u : 0u;
-        qq = q - neg;
-        cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
+        div_norm(head, norm, rcp_norm, qq, cf);
     }
     // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket
     __device__ __forceinline__ void lookup(const unsigned char* bkt, uint32_t shift) {
@@ -626,23 +637,10 @@ struct DecChainG {
     }
     __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
         form_window();
-        const uint32_t h1 = hi32(head), h0 = lo32(head);
-        const uint32_t js = static_cast<uint32_t>(__builtin_clzll(head | 1)) >> 3;
-        const uint32_t sh = 4u - js;
-        const uint32_t xj1 = ab(h1, h0, sh), xj0 = ab(h0, W, sh);
-        const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
-        const bool one_less = mk64(xm1, xm0) >= L;
-        const bool keep = h1 >= (1u << 24);
-        const uint32_t k = keep ? 0u : js - (one_less ? 1u : 0u);
-        head = keep ? head : (one_less ? mk64(xm1, xm0) : mk64(xj1, xj0));
-        P -= static_cast<int32_t>(k);
-        read_window();
+        P -= static_cast<int32_t>(renorm_up(head, W, L));
+        read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        uint64_t q = qest(head, rcp_norm);
-        const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
-        const uint32_t neg = ii < 0 ? 1u : 0u;
-        qq = q - neg;
-        cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
+        div_norm(head, norm, rcp_norm, qq, cf);
     }
     __device__ __forceinline__ void lookup(const DecBucketG* __restrict__ bkt, uint32_t shift) {
         const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
