@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libshufflecoding_amd.so")
+# SHUFFLE_CODING_AMD_LIB selects another build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("SHUFFLE_CODING_AMD_LIB") or os.path.join(HERE, "lib", "libshufflecoding_amd.so")
 
 ANS_OK, ANS_E_ZERO_MASS, ANS_E_EXHAUSTED, ANS_E_LEN, ANS_E_SYMBOL = 0, 1, 2, 3, 4
 ANS_E_NORM_RANGE, ANS_E_DEVICE, ANS_E_ALLOC, ANS_E_ARG, ANS_E_MISMATCH = 5, 6, 7, 8, 9

@@ -486,6 +486,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     const uint32_t shift = t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
+#ifdef ANS_PAD_VALU
+    uint32_t pad_acc = threadIdx.x;
+#endif
     DecChain ch;
     ch.ring = reinterpret_cast<uint32_t*>(lds + kDecTableBytes) + threadIdx.x;
     ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
@@ -508,6 +511,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
                 ch.point();
             }
             ch.renorm_div(L, norm, rcp_norm);
+#ifdef ANS_PAD_VALU  // experiment: independent filler VALU per symbol (issue- vs latency-bound)
+#pragma unroll
+            for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));
+#endif
             ch.lookup(tab, shift);
             if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
             ch.update();
@@ -533,6 +540,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     const int32_t remaining = ch.P + 4;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+#ifdef ANS_PAD_VALU
+    if (pad_acc == 0xDEADBEEFu) atomicOr(status, 1u << 31);
+#endif
 }
 
 // ====================================================================== decode, large alphabets
