@@ -46,6 +46,13 @@ __device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
     __builtin_nontemporal_store(v4u32{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u32*>(p));
 }
 
+// LDS accesses by byte offset (address space 3): keeps the address arithmetic in 32 bits
+// where the compiler otherwise adds the (zero) LDS base or splits constants out of offsets.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t off) { return *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(off)); }
+__device__ __forceinline__ uint64_t lds_ld64(uint32_t off) { return *reinterpret_cast<const lds_u64*>(static_cast<uintptr_t>(off)); }
+
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
@@ -339,7 +346,7 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
 // ====================================================================== decode
 // One decode chain = one chunk, read from the end.  P is the stream position minus 4: the
 // window W = stream bytes [P, P+4) (byte P+3 on top) comes from ring dwords y = P>>2 and y+1
-// with one v_alignbyte.  The ring (after the tables, at kDecTableBytes) is [row][lane] with kDecRows = 33 rows:
+// with one v_alignbyte.  The ring (LDS offset 0; tables after it) is [row][lane] with kDecRows = 33 rows:
 // row 32 mirrors row 0, so y and y+1 are one ds_read2st64_b32 even across the wrap.  Pages
 // (16 rows) land at points: page low+1 is free once dword y+1 lies in page low, and the page
 // below `low` is always in flight in registers (S); pages below 0 are zeros (the Zeros
@@ -382,12 +389,13 @@ struct DecChain {
             for (int k = 0; k < 4; ++k) S[k] = make_uint4(0, 0, 0, 0);
         }
     }
-    // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0)
-    uint32_t wx, wy;
+    // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
+    // ring at LDS offset 0 the row address is one v_and_or of (P << 9) and the lane's column.
+    uint32_t wx, wy, col;  // col = 4 * lane: the lane's byte column in the ring (LDS offset 0)
     __device__ __forceinline__ void read_window() {
-        const uint32_t* a = ring + ((static_cast<uint32_t>(P) >> 2) & 31u) * kBlock;
-        wy = a[0];
-        wx = a[kBlock];
+        const uint32_t a = ((static_cast<uint32_t>(P) << 9) & 0xF800u) | col;  // row (P>>2)&31
+        wy = lds_ld32(a);
+        wx = lds_ld32(a + 4 * kBlock);
     }
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P) & 3u); }
     // the top two pages land before decoding starts; the third is requested
@@ -431,9 +439,12 @@ struct DecChain {
         div_norm(head, norm, rcp_norm, qq, cf);
     }
     // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket
-    __device__ __forceinline__ void lookup(const unsigned char* bkt, uint32_t shift) {
-        const uint64_t* e = reinterpret_cast<const uint64_t*>(bkt + __umul24(cf >> shift, sizeof(DecBucket)));
-        uint64_t r01 = e[0], r23 = e[1], r4s = e[2];
+    __device__ __forceinline__ void lookup(const unsigned char* lds, uint32_t shift) {
+        // bucket address = (cf >> shift) * 24 + table base: one v_mad_u32_u24 (kept whole: the
+        // compiler otherwise splits the base out into two adds, as it exceeds the ds offset)
+        uint32_t off;
+        asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(off) : "v"(cf >> shift), "s"(kDecRingBytes));
+        uint64_t r01 = lds_ld64(off), r23 = lds_ld64(off + 8), r4s = lds_ld64(off + 16);
         // all three reads complete here: the compiler otherwise defers the ones a select needs
         // only on some lanes into branches, adding dependent LDS round trips
         asm volatile("" ::"v"(r01), "v"(r23), "v"(r4s));
@@ -443,6 +454,7 @@ struct DecChain {
         cum = b3 ? e23.y : (b2 ? e23.x : (b1 ? e01.y : e01.x));
         nxt = b3 ? e4s.x : (b2 ? e23.y : (b1 ? e23.x : e01.y));
         sx = e4s.y + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
+        asm volatile("" : "+v"(sx));  // now, not at the unit's end (its compare masks would spill)
         far = cf >= e4s.x;
     }
     __device__ __forceinline__ void lookup_far(const uint32_t* lcum) {  // 4+ boundaries in the bucket
@@ -458,13 +470,14 @@ struct DecChain {
 };
 
 // SPP: symbols per point (U, or U/2 when U*KMAX > 60: u8 tables whose pops can take 4 bytes).
-template <typename Sym, int SPP>
+// kFar: some bucket holds more than four cdf boundaries, so the voted slow path is compiled in.
+template <typename Sym, int SPP, bool kFar>
 __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
                                                       uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
-    unsigned char* tab = lds;  // tables at offset 0 (immediate ds offsets), ring after
+    unsigned char* tab = lds + kDecRingBytes;  // ring at offset 0, tables after it
     {
         uint2* b = reinterpret_cast<uint2*>(tab);
         const uint2* gb = reinterpret_cast<const uint2*>(t.dbkt);
@@ -490,7 +503,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     uint32_t pad_acc = threadIdx.x;
 #endif
     DecChain ch;
-    ch.ring = reinterpret_cast<uint32_t*>(lds + kDecTableBytes) + threadIdx.x;
+    ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
+    ch.col = 4 * threadIdx.x;
     ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 
@@ -510,13 +524,14 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
                 }
                 ch.point();
             }
+            __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
             ch.renorm_div(L, norm, rcp_norm);
 #ifdef ANS_PAD_VALU  // experiment: independent filler VALU per symbol (issue- vs latency-bound)
 #pragma unroll
             for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));
 #endif
-            ch.lookup(tab, shift);
-            if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+            ch.lookup(lds, shift);
+            if (kFar && __builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
             ch.update();
             put_sym<Sym>(outv, j, ch.sx);
         }

@@ -405,10 +405,13 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
                 fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
-            if (U * ft.kmax > 60)
-                fast::k_decode<Sym, U / 2><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
-            else
-                fast::k_decode<Sym, U><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+#define DEC(SPP, FAR) fast::k_decode<Sym, SPP, FAR><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
+            if (U * ft.kmax > 60) {
+                if (ft.dec_far) DEC(U / 2, true); else DEC(U / 2, false);
+            } else {
+                if (ft.dec_far) DEC(U, true); else DEC(U, false);
+            }
+#undef DEC
         }
         HIP_TRY(hipGetLastError());
     }
@@ -502,6 +505,9 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             DecBucket& d = dec[j];
             for (int i = 0; i < 5; ++i) d.c[i] = cum[s0 + i];
             d.s0 = s0;
+            // every cf of the bucket below cdf(s0 + 4)?  (the last bucket ends at norm)
+            const uint64_t end = std::min<uint64_t>(t.norm, (static_cast<uint64_t>(j) + 1) << shift);
+            if (d.c[4] < end) ft.dec_far = 1;
         } else {
             DecBucketG& d = decg[j];
             for (int i = 0; i < 6; ++i) d.c[i] = cum[s0 + i];

@@ -86,6 +86,7 @@ struct FastTable {
     uint32_t enc_global;  // rows read from global memory (nsym > 256; ans_fast.hpp kGlobalRows)
     uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
     uint32_t dec_global;  // decode fast path for nsym > 256 (k_decode_g, buckets in global memory)
+    uint32_t dec_far;     // some LDS bucket holds more than four cdf boundaries (slow path needed)
 };
 
 }  // namespace shuffle_coding
