@@ -33,6 +33,7 @@ constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 constexpr uint32_t kEncMcOffset = 8 * 257;  // encode LDS: rcp[257] then (mass, cum)[257]
 constexpr uint32_t kEncLdsBytes = 2 * kEncMcOffset;
+constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB at LDS offset 0
 constexpr uint32_t kDecTableBytes = 14336;  // decode buckets in LDS: 2 x (66 KiB ring + 14 KiB) per CU
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
@@ -45,13 +46,6 @@ __device__ __forceinline__ uint4 nt_load(const uint4* p) {
 __device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
     __builtin_nontemporal_store(v4u32{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u32*>(p));
 }
-
-// LDS accesses by byte offset (address space 3): keeps the address arithmetic in 32 bits
-// where the compiler otherwise adds the (zero) LDS base or splits constants out of offsets.
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) uint64_t lds_u64;
-__device__ __forceinline__ uint32_t lds_ld32(uint32_t off) { return *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(off)); }
-__device__ __forceinline__ uint64_t lds_ld64(uint32_t off) { return *reinterpret_cast<const lds_u64*>(static_cast<uintptr_t>(off)); }
 
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
@@ -75,10 +69,19 @@ __device__ __forceinline__ uint64_t qest(uint64_t x, double rcp) {
 }
 
 // Lane-private ring of 32 dwords in a [dword][lane] image.
+// LDS accesses by byte offset (address space 3): keeps the address arithmetic in 32 bits
+// where the compiler otherwise adds the (zero) LDS base or splits constants out of offsets.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t off) { return *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(off)); }
+__device__ __forceinline__ uint64_t lds_ld64(uint32_t off) { return *reinterpret_cast<const lds_u64*>(static_cast<uintptr_t>(off)); }
+
+// (kept at LDS offset 0: a row address is one v_and_or of the row bits and the lane's column)
 struct Ring {
-    uint32_t* base;  // &image[0][lane]
-    __device__ __forceinline__ uint32_t& at(int32_t i) const {
-        return base[(static_cast<uint32_t>(i) & 31u) * kBlock];
+    uint32_t col;  // 4 * lane
+    __device__ __forceinline__ lds_u32& at(int32_t i) const {
+        const uint32_t a = ((static_cast<uint32_t>(i) << 11) & 0xF800u) | col;
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a));
     }
 };
 
@@ -151,8 +154,9 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     extern __shared__ __align__(16) unsigned char lds[];
     // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
     // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
-    double* rcps = reinterpret_cast<double*>(lds);
-    uint2* mcs = reinterpret_cast<uint2*>(lds + kEncMcOffset);  // fixed offset: immediate ds offsets
+    // ring at offset 0 (64 KiB), rows after it
+    double* rcps = reinterpret_cast<double*>(lds + kEncRingBytes);
+    uint2* mcs = reinterpret_cast<uint2*>(lds + kEncRingBytes + kEncMcOffset);  // immediate ds offset from rcps
     if (!kGlobalRows) {
         for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) {
             const EncRow r = t.enc[i];
@@ -161,10 +165,12 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         }
     }
     auto row = [&](uint32_t s) __attribute__((always_inline)) {
-        const uint2 mc = mcs[s];
-        return EncRow{rcps[s], mc.x, mc.y};
+        uint32_t off;  // 8*s + table base in one v_lshl_add (the base exceeds the ds offset field)
+        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(off) : "v"(s), "s"(kEncRingBytes));
+        const uint64_t mc = lds_ld64(off + kEncMcOffset);
+        return EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
     };
-    const Ring ring{reinterpret_cast<uint32_t*>(lds + t.enc_lds_bytes) + threadIdx.x};
+    const Ring ring{4 * threadIdx.x};
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;
