@@ -31,8 +31,9 @@ namespace fast {
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
-constexpr uint32_t kEncMcOffset = 8 * 257;  // encode LDS: rcp[257] then (mass, cum)[257]
-constexpr uint32_t kEncLdsBytes = 2 * kEncMcOffset;
+constexpr uint32_t kEncMcOffset = 8 * 257;  // encode LDS: rcp[257], (mass, cum)[257], p*K[257]
+constexpr uint32_t kEncPkOffset = 2 * kEncMcOffset;
+constexpr uint32_t kEncLdsBytes = (3 * kEncMcOffset + 15) & ~15u;
 constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB at LDS offset 0
 constexpr uint32_t kDecTableBytes = 14336;  // decode buckets in LDS: 2 x (66 KiB ring + 14 KiB) per CU
 constexpr uint64_t kMaxMinHead = 1ull << 56;
@@ -157,18 +158,26 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     // ring at offset 0 (64 KiB), rows after it
     double* rcps = reinterpret_cast<double*>(lds + kEncRingBytes);
     uint2* mcs = reinterpret_cast<uint2*>(lds + kEncRingBytes + kEncMcOffset);  // immediate ds offset from rcps
+    uint64_t* pks = reinterpret_cast<uint64_t*>(lds + kEncRingBytes + kEncPkOffset);
     if (!kGlobalRows) {
         for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) {
             const EncRow r = t.enc[i];
             rcps[i] = r.rcp;
             mcs[i] = make_uint2(r.mass, r.cum);
+            pks[i] = static_cast<uint64_t>(r.mass) * t.K;  // renorm bound p*K (src/ans.rs:100)
         }
     }
+    // a row in registers: the table row plus its renorm bound p*K (read from LDS, or formed)
+    struct Row {
+        EncRow e;
+        uint64_t pK;
+    };
     auto row = [&](uint32_t s) __attribute__((always_inline)) {
         uint32_t off;  // 8*s + table base in one v_lshl_add (the base exceeds the ds offset field)
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(off) : "v"(s), "s"(kEncRingBytes));
         const uint64_t mc = lds_ld64(off + kEncMcOffset);
-        return EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
+        return Row{EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)},
+                   lds_ld64(off + kEncPkOffset)};
     };
     const Ring ring{4 * threadIdx.x};
     __syncthreads();
@@ -199,11 +208,12 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             ++fp;
         }
     };
-    auto push_one = [&](const EncRow& e) __attribute__((always_inline)) {
+    auto bound = [&](const EncRow& e) __attribute__((always_inline)) {
+        return kK32 ? static_cast<uint64_t>(e.mass) * static_cast<uint32_t>(K) : static_cast<uint64_t>(e.mass) * K;
+    };
+    auto push_one = [&](const EncRow& e, uint64_t pK) __attribute__((always_inline)) {
         asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
         // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
-        const uint64_t pK = kK32 ? static_cast<uint64_t>(e.mass) * static_cast<uint32_t>(K)
-                                 : static_cast<uint64_t>(e.mass) * K;
         uint32_t k = (head >> 8) >= pK ? 1u : 0u;
         if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 1u : 0u;
         if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 1u : 0u;
@@ -223,13 +233,13 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto process = [&](const uint4& unit) __attribute__((always_inline)) {
         // rows are read one symbol ahead; the scheduling barriers keep the compiler from
         // hoisting all sixteen reads (and their registers) to the top of the unit
-        EncRow e_next = row(min(sym_of<Sym>(unit, U - 1), sentinel));
+        Row e_next = row(min(sym_of<Sym>(unit, U - 1), sentinel));
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             __builtin_amdgcn_sched_barrier(0);
-            const EncRow e = e_next;
+            const Row e = e_next;
             if (j > 0) e_next = row(min(sym_of<Sym>(unit, j - 1), sentinel));
-            push_one(e);
+            push_one(e.e, e.pK);
         }
     };
     auto request_rows = [&](const uint4& unit, EncRow* buf) __attribute__((always_inline)) {
@@ -238,7 +248,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     };
     auto process_rows = [&](const EncRow* buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = U - 1; j >= 0; --j) push_one(buf[j]);
+        for (int j = U - 1; j >= 0; --j) push_one(buf[j], bound(buf[j]));
     };
 
     // (non-temporal symbol loads / page stores measured 28% SLOWER with rows in global memory)
