@@ -119,13 +119,22 @@ int ans_gpu_device_count(int *count);
 /* one context per device; owns a HIP stream */
 int ans_gpu_create(int device, ans_gpu **out);
 void ans_gpu_free(ans_gpu *g);
+/* Page-locked host memory for the host-buffer calls below (hipHostMalloc): their copies
+ * then run asynchronously and overlap; pageable buffers go through the runtime's staging. */
+int ans_host_alloc(size_t bytes, void **out);
+void ans_host_free(void *p);
+/* Symbol bytes per batch of the host-buffer pipeline below (0 = the default, 256 MiB).
+ * Batches overlap their H2D copy, kernels and D2H copy on separate streams. */
+int ans_gpu_set_batch_bytes(ans_gpu *g, uint64_t batch_bytes);
 /* uploads the table (and its derived reciprocal / icdf-bucket data) to the device */
 int ans_gpu_table_create(ans_gpu *g, const ans_table *t, ans_gpu_table **out);
 void ans_gpu_table_free(ans_gpu_table *gt);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);
 
-/* Host buffers in, host buffers out (synchronous; includes H2D/D2H).
+/* Host buffers in, host buffers out (synchronous; includes H2D/D2H), pipelined in batches
+ * of chunks over a persistent device workspace.  Page-locked host buffers let the copies
+ * run asynchronously; pageable ones still work (the runtime stages them).
  * Encode writes the streams densely: chunk j at out[offsets[j] .. offsets[j]+lens[j]).
  * out_cap must hold the total (query the exact total by passing out == NULL: *total is
  * set and nothing else is written). */

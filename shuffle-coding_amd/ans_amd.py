@@ -68,6 +68,9 @@ SIGNATURES = {
     "ans_gpu_device_count": (ci, [ctypes.POINTER(ci)]),
     "ans_gpu_create": (ci, [ci, ctypes.POINTER(vp)]),
     "ans_gpu_free": (None, [vp]),
+    "ans_gpu_set_batch_bytes": (ci, [vp, u64]),
+    "ans_host_alloc": (ci, [sz, ctypes.POINTER(vp)]),
+    "ans_host_free": (None, [vp]),
     "ans_gpu_table_create": (ci, [vp, vp, ctypes.POINTER(vp)]),
     "ans_gpu_table_free": (None, [vp]),
     "ans_gpu_slot_capacity": (ci, [vp, u64, u64p]),
@@ -481,6 +484,10 @@ class Gpu:
             _lib.ans_gpu_free(h)
             self.h = None
 
+    def set_batch_bytes(self, batch_bytes):
+        """Symbol bytes per batch of the host-buffer pipeline (0 = default, 256 MiB)."""
+        _check(lib().ans_gpu_set_batch_bytes(self.h, batch_bytes), "ans_gpu_set_batch_bytes")
+
     def status(self, d_status, stream=None):
         st = ci(0)
         _check(lib().ans_dev_status(self.h, _dptr(d_status), _sptr(stream), ctypes.byref(st)), "ans_dev_status")
@@ -489,6 +496,31 @@ class Gpu:
     def compact(self, d_slots, slot_cap, d_lens, d_offsets, nchunks, d_out, stream=None):
         _check(lib().ans_dev_compact(self.h, _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_offsets), nchunks,
                                      _dptr(d_out), _sptr(stream)), "ans_dev_compact")
+
+
+class _PinnedBlock:
+    """Owns one ans_host_alloc block; freed when the last numpy view of it goes away."""
+
+    def __init__(self, nbytes):
+        h = vp()
+        _check(lib().ans_host_alloc(max(nbytes, 1), ctypes.byref(h)), "ans_host_alloc")
+        self.ptr = h.value
+        self.nbytes = nbytes
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.ans_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_empty(n, dtype=np.uint8):
+    """A numpy array in page-locked host memory (ans_host_alloc): host-buffer GPU calls on
+    it overlap their copies with the kernels."""
+    dtype = np.dtype(dtype)
+    blk = _PinnedBlock(n * dtype.itemsize)
+    buf = (ctypes.c_char * max(n * dtype.itemsize, 1)).from_address(blk.ptr)
+    buf._owner = blk  # keeps the block alive as long as any view of the buffer
+    return np.frombuffer(buf, dtype=dtype, count=n)
 
 
 def _dptr(t):
@@ -539,9 +571,8 @@ class GpuTable:
         n = len(syms)
         nchunks = -(-n // chunk_len)
         total = u64(0)
-        _check(lib().ans_gpu_encode_chunks(self.h, _np_ptr(syms), w, n, chunk_len, None, 0, None, None,
-                                           ctypes.byref(total)), "ans_gpu_encode_chunks(size)")
-        out = np.zeros(max(total.value, 1), np.uint8)
+        # one pass into a worst-case buffer (slot capacity per chunk bounds every stream)
+        out = np.empty(max(nchunks * self.slot_capacity(chunk_len), 1), np.uint8)
         offsets = np.zeros(max(nchunks, 1), np.uint64)
         lens = np.zeros(max(nchunks, 1), np.uint64)
         _check(lib().ans_gpu_encode_chunks(self.h, _np_ptr(syms), w, n, chunk_len, _np_ptr(out), len(out),

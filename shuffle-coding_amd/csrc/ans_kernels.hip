@@ -12,8 +12,11 @@
 //   table    : DevSym[nsym+1] (+ u16 icdf buckets), staged into LDS when it fits.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "ans_fast.hpp"
@@ -21,9 +24,42 @@
 
 using namespace shuffle_coding;
 
+// Host-buffer pipeline (ans_gpu_encode_chunks / ans_gpu_decode_chunks): batches of chunks
+// flow through kPipeDepth workspace slots, so that the H2D copy of batch b+1, the kernels of
+// batch b and the D2H copy of batch b-1 overlap.  Kernels alternate between
+// two compute streams (the context's and s_comp2): a batch's kernels occupy few CUs for about
+// one chain latency (~1 ms for 4096-symbol chunks), so consecutive batches must overlap too.
+// Four streams in all, the per-process hardware queue count.  The workspace persists in the
+// context and grows on demand.
+constexpr int kPipeDepth = 3;
+struct PipeSlot {
+    void* d_syms = nullptr;     // batch symbols
+    uint8_t* d_slots = nullptr; // batch streams in the slot layout
+    uint8_t* d_dense = nullptr; // batch streams, dense (encode output / decode input)
+    uint32_t* d_lens = nullptr;
+    uint64_t* d_offs = nullptr;  // batch offsets (+ total at [nchunks] after encode)
+    uint32_t* h_lens = nullptr;  // pinned staging
+    uint64_t* h_offs = nullptr;  // pinned staging
+    hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_meta = nullptr, ev_out = nullptr;
+    bool used = false;
+};
+struct HostPipe {
+    hipStream_t s_in = nullptr, s_out = nullptr, s_comp2 = nullptr;
+    PipeSlot slot[kPipeDepth];
+    uint32_t* d_status = nullptr;
+    size_t cap_syms = 0, cap_slots = 0, cap_dense = 0, cap_chunks = 0;  // per slot
+    // page-locked callers (device-driven copies): per-call chunk metadata and the carry
+    uint64_t* h_meta = nullptr;  // mapped host staging: offsets[nchunks], lens[nchunks]
+    size_t cap_meta = 0;
+    uint64_t* d_acc = nullptr;   // running container offset across batches
+    hipEvent_t ev_scan = nullptr;
+};
+
 struct ans_gpu {
     int device;
     hipStream_t stream;
+    HostPipe* pipe;
+    uint64_t batch_bytes;  // symbol bytes per pipeline batch (0 = default)
 };
 
 struct ans_gpu_table {
@@ -290,6 +326,26 @@ __global__ __launch_bounds__(kBlock) void k_gen_iid(DevTable t, uint64_t seed, u
     }
 }
 
+// One wave copies one stream: byte head until dst is dword-aligned, then aligned dword
+// stores funnelled from two source dwords (v_alignbyte), then the byte tail.  Reads up to 4
+// bytes past the source stream, which every caller's buffer has as slack.
+__device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
+                                          uint32_t lane) {
+    const uint32_t head = min(len, (4u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst) & 3)) & 3u);
+    if (lane < head) dst[lane] = src[lane];
+    dst += head;
+    src += head;
+    len -= head;
+    const uint32_t nd = len / 4, sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 3);
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+    for (uint32_t i = lane; i < nd; i += 64) {
+        const uint32_t lo = s4[i], hi = s4[i + 1];
+        d4[i] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+    if (lane < len - 4 * nd) dst[4 * nd + lane] = src[4 * nd + lane];
+}
+
 // One wave per chunk copies its slot into the dense container.
 __global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                     const uint32_t* __restrict__ lens,
@@ -300,7 +356,7 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ 
     if (c >= nchunks) return;
     const uint8_t* s = slots + c * slot_cap;
     uint8_t* d = out + offsets[c];
-    for (uint32_t k = lane; k < lens[c]; k += 64) d[k] = s[k];
+    wave_copy(d, s, lens[c], lane);
 }
 
 // One wave per chunk copies a dense-container stream into its slot (the inverse of k_compact).
@@ -312,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint8_t* __restrict__ i
     if (c >= nchunks) return;
     const uint8_t* s = in + offsets[c];
     uint8_t* d = slots + c * slot_cap;
-    for (uint32_t k = lane; k < lens[c]; k += 64) d[k] = s[k];
+    wave_copy(d, s, lens[c], lane);
 }
 
 // ------------------------------------------------------------------ launch helpers
@@ -550,6 +606,584 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     return ANS_OK;
 }
 
+// ------------------------------------------------------------------ host-buffer pipeline
+
+constexpr int kPipeScattered = -1;
+
+// Exclusive scan of a batch's stream lengths: offs[j] = sum of lens[0..j), offs[n] = total.
+// One workgroup (n <= a few 10^5 per batch): each thread sums a contiguous segment, the
+// segment sums are scanned in LDS, then each thread writes its segment's offsets.
+__global__ __launch_bounds__(1024) void k_scan_lens(const uint32_t* __restrict__ lens, uint64_t n,
+                                                    uint64_t* __restrict__ offs) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint64_t per = (n + 1023) / 1024, b = t * per, e = b + per < n ? b + per : n;
+    uint64_t sum = 0;
+    for (uint64_t i = b; i < e; ++i) sum += lens[i];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint64_t i = b; i < e; ++i) {
+        offs[i] = run;
+        run += lens[i];
+    }
+    if (t == 1023) offs[n] = part[1023];
+}
+
+// Like k_expand, with the batch's dense bytes starting at container offset `base`.
+__global__ __launch_bounds__(kBlock) void k_expand_based(const uint8_t* __restrict__ in,
+                                                         const uint64_t* __restrict__ offsets, uint64_t base,
+                                                         const uint32_t* __restrict__ lens, uint64_t nchunks,
+                                                         uint8_t* __restrict__ slots, uint64_t slot_cap) {
+    const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
+    const uint8_t* s = in + (offsets[c] - base);
+    uint8_t* d = slots + c * slot_cap;
+    wave_copy(d, s, lens[c], lane);
+}
+
+void pipe_release(HostPipe* p) {
+    for (PipeSlot& s : p->slot) {
+        (void)hipFree(s.d_syms);
+        (void)hipFree(s.d_slots);
+        (void)hipFree(s.d_dense);
+        (void)hipFree(s.d_lens);
+        (void)hipFree(s.d_offs);
+        (void)hipHostFree(s.h_lens);
+        (void)hipHostFree(s.h_offs);
+        s.d_syms = s.d_slots = s.d_dense = nullptr;
+        s.d_syms = nullptr;
+        s.d_lens = nullptr;
+        s.d_offs = nullptr;
+        s.h_lens = nullptr;
+        s.h_offs = nullptr;
+        s.used = false;
+    }
+    p->cap_syms = p->cap_slots = p->cap_dense = p->cap_chunks = 0;
+}
+
+void pipe_free(ans_gpu* g) {
+    HostPipe* p = g->pipe;
+    if (!p) return;
+    (void)hipDeviceSynchronize();
+    pipe_release(p);
+    for (PipeSlot& s : p->slot) {
+        (void)hipEventDestroy(s.ev_in);
+        (void)hipEventDestroy(s.ev_comp);
+        (void)hipEventDestroy(s.ev_meta);
+        (void)hipEventDestroy(s.ev_out);
+    }
+    (void)hipFree(p->d_status);
+    (void)hipFree(p->d_acc);
+    if (p->h_meta) (void)hipHostFree(p->h_meta);
+    if (p->ev_scan) (void)hipEventDestroy(p->ev_scan);
+    (void)hipStreamDestroy(p->s_in);
+    (void)hipStreamDestroy(p->s_out);
+    (void)hipStreamDestroy(p->s_comp2);
+    delete p;
+    g->pipe = nullptr;
+}
+
+// The context's pipeline with per-slot room for `syms` symbol bytes, `slots` slot bytes,
+// `dense` dense bytes and `chunks` chunks (reallocated, after draining, when it must grow).
+int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks, HostPipe** out) {
+    if (!g->pipe) {
+        auto* p = new (std::nothrow) HostPipe{};
+        if (!p) return ANS_E_ALLOC;
+        g->pipe = p;
+        HIP_TRY(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&p->s_comp2, hipStreamNonBlocking));
+        for (PipeSlot& s : p->slot) {
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_comp, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_meta, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_out, hipEventDisableTiming));
+        }
+        HIP_TRY(hipMalloc(&p->d_status, sizeof(uint32_t)));
+    }
+    HostPipe* p = g->pipe;
+    if (syms > p->cap_syms || slots > p->cap_slots || dense > p->cap_dense || chunks > p->cap_chunks) {
+        HIP_TRY(hipDeviceSynchronize());
+        syms = std::max(syms, p->cap_syms);
+        slots = std::max(slots, p->cap_slots);
+        dense = std::max(dense, p->cap_dense);
+        chunks = std::max(chunks, p->cap_chunks);
+        pipe_release(p);
+        for (PipeSlot& s : p->slot) {
+            HIP_TRY(hipMalloc(&s.d_syms, syms + 16));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_slots), slots + 16));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dense), dense + 16));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_lens), sizeof(uint32_t) * chunks + 16));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_offs), sizeof(uint64_t) * (chunks + 1) + 16));
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_lens), sizeof(uint32_t) * chunks + 16));
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_offs), sizeof(uint64_t) * (chunks + 1) + 16));
+        }
+        p->cap_syms = syms;
+        p->cap_slots = slots;
+        p->cap_dense = dense;
+        p->cap_chunks = chunks;
+    }
+    for (PipeSlot& s : p->slot) s.used = false;
+    *out = p;
+    return ANS_OK;
+}
+
+// Chunks per batch: about batch_bytes (default 256 MiB) of symbols.  A batch's kernels take
+// about one chain latency (~1 ms) whatever its size until it fills the GPU, so batches must
+// be large; 256 MiB measured best for the round trip.
+constexpr uint64_t kPipeBatchBytes = 256ull << 20;
+uint64_t pipe_batch_chunks(const ans_gpu* g, uint64_t nchunks, uint64_t chunk_bytes) {
+    const uint64_t target = g->batch_bytes ? g->batch_bytes : kPipeBatchBytes;
+    uint64_t b = target / (chunk_bytes ? chunk_bytes : 1);
+    if (b < 1) b = 1;
+    return b < nchunks ? b : nchunks;
+}
+
+// Encode from host symbols into a host dense container.  Batch b: H2D (s_in) -> encode,
+// length scan, compaction, lengths D2H (compute stream b & 1); the host waits for batch
+// b-1's lengths only after batch b is queued, then queues b-1's dense D2H (s_out) at its
+// running offset.  With out == NULL (size query) nothing but the lengths comes back.
+template <typename Sym>
+int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_len, uint8_t* out, uint64_t out_cap,
+                uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+    constexpr uint64_t w = sizeof(Sym);
+    const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    uint64_t slot_cap = 0;
+    ans_gpu_slot_capacity(gt, chunk_len, &slot_cap);
+    const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
+    HostPipe* p = nullptr;
+    int rc = pipe_get(gt->g, B * chunk_len * w, B * slot_cap, out ? B * slot_cap : 0, B, &p);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(p->d_status, 0, sizeof(uint32_t), gt->g->stream));
+    HIP_TRY(hipStreamSynchronize(gt->g->stream));
+    const uint64_t nbatch = (nchunks + B - 1) / B;
+    const auto* src = static_cast<const uint8_t*>(syms);
+    bool copy = out != nullptr;
+    int len_err = ANS_OK;
+    uint64_t acc = 0;
+    auto enqueue = [&](uint64_t b) -> int {
+        PipeSlot& s = p->slot[b % kPipeDepth];
+        const hipStream_t sc = (b & 1) ? p->s_comp2 : gt->g->stream;
+        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
+        const uint64_t nb = std::min(n - n0, nc * chunk_len);
+        if (s.used) HIP_TRY(hipStreamWaitEvent(p->s_in, s.ev_comp, 0));  // symbols of batch b - depth consumed
+        HIP_TRY(hipMemcpyAsync(s.d_syms, src + n0 * w, nb * w, hipMemcpyHostToDevice, p->s_in));
+        HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
+        HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
+        if (s.used) HIP_TRY(hipStreamWaitEvent(sc, s.ev_out, 0));  // dense bytes of batch b - depth copied out
+        int r = launch_encode<Sym>(gt, s.d_syms, nb, chunk_len, s.d_slots, slot_cap, s.d_lens, p->d_status, sc);
+        if (r) return r;
+        k_scan_lens<<<1, 1024, 0, sc>>>(s.d_lens, nc, s.d_offs);
+        HIP_TRY(hipGetLastError());
+        if (copy) {
+            k_compact<<<grid_for(nc * 64), kBlock, 0, sc>>>(s.d_slots, slot_cap, s.d_lens, s.d_offs, nc, s.d_dense);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipEventRecord(s.ev_comp, sc));
+        HIP_TRY(hipMemcpyAsync(s.h_lens, s.d_lens, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, sc));
+        HIP_TRY(hipMemcpyAsync(s.h_offs, s.d_offs + nc, sizeof(uint64_t), hipMemcpyDeviceToHost, sc));
+        HIP_TRY(hipEventRecord(s.ev_meta, sc));
+        s.used = true;
+        return ANS_OK;
+    };
+    auto finish = [&](uint64_t b) -> int {
+        PipeSlot& s = p->slot[b % kPipeDepth];
+        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0);
+        HIP_TRY(hipEventSynchronize(s.ev_meta));
+        const uint64_t bt = s.h_offs[0];
+        if (copy && acc + bt > out_cap) {
+            copy = false;  // keep coding to report the exact total
+            len_err = ANS_E_LEN;
+        }
+        if (copy && bt) HIP_TRY(hipMemcpyAsync(out + acc, s.d_dense, bt, hipMemcpyDeviceToHost, p->s_out));
+        HIP_TRY(hipEventRecord(s.ev_out, p->s_out));
+        uint64_t o = acc;
+        for (uint64_t j = 0; j < nc; ++j) {
+            if (out) {
+                offsets[c0 + j] = o;
+                lens[c0 + j] = s.h_lens[j];
+            }
+            o += s.h_lens[j];
+        }
+        acc = o;
+        return ANS_OK;
+    };
+    for (uint64_t b = 0; b < nbatch; ++b) {
+        if ((rc = enqueue(b))) return rc;
+        if (b > 0 && (rc = finish(b - 1))) return rc;
+    }
+    if (nbatch && (rc = finish(nbatch - 1))) return rc;
+    HIP_TRY(hipStreamSynchronize(p->s_out));
+    HIP_TRY(hipStreamSynchronize(p->s_comp2));
+    int st = 0;
+    if ((rc = ans_dev_status(gt->g, p->d_status, gt->g->stream, &st))) return rc;
+    if (st) return st;
+    *total = acc;
+    return len_err;
+}
+
+// Decode a host dense container into host symbols.  Batch b: its byte span and rebased
+// offsets/lengths H2D (s_in) -> expansion into the slot layout and decode (compute stream
+// b & 1) ->
+// symbols D2H (s_out).  No host synchronisation inside the loop beyond staging reuse.
+// Returns kPipeScattered when some batch's streams spread over more than twice its slot bytes
+// (a container that is not dense); the caller then takes the whole-buffer path.
+template <typename Sym>
+int pipe_decode(ans_gpu_table* gt, const uint8_t* in, const uint64_t* offsets, const uint32_t* l32, uint64_t slot_cap,
+                uint64_t n, uint64_t chunk_len, int gen_kind, void* out) {
+    constexpr uint64_t w = sizeof(Sym);
+    const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
+    const uint64_t nbatch = (nchunks + B - 1) / B;
+    std::vector<uint64_t> lo(nbatch), span(nbatch);
+    uint64_t max_span = 0;
+    for (uint64_t b = 0; b < nbatch; ++b) {
+        const uint64_t c0 = b * B, c1 = std::min(nchunks, c0 + B);
+        uint64_t l = ~0ull, h = 0;
+        for (uint64_t j = c0; j < c1; ++j) {
+            l = std::min(l, offsets[j]);
+            h = std::max(h, offsets[j] + l32[j]);
+        }
+        lo[b] = l;
+        span[b] = h - l;
+        max_span = std::max(max_span, span[b]);
+    }
+    if (max_span > 2 * B * slot_cap) return kPipeScattered;
+    HostPipe* p = nullptr;
+    int rc = pipe_get(gt->g, B * chunk_len * w, B * slot_cap, max_span, B, &p);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(p->d_status, 0, sizeof(uint32_t), gt->g->stream));
+    HIP_TRY(hipStreamSynchronize(gt->g->stream));
+    auto* dst = static_cast<uint8_t*>(out);
+    for (uint64_t b = 0; b < nbatch; ++b) {
+        PipeSlot& s = p->slot[b % kPipeDepth];
+        const hipStream_t sc = (b & 1) ? p->s_comp2 : gt->g->stream;
+        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
+        const uint64_t nb = std::min(n - n0, nc * chunk_len);
+        if (s.used) {
+            HIP_TRY(hipEventSynchronize(s.ev_in));  // staging of batch b - depth uploaded
+            HIP_TRY(hipStreamWaitEvent(p->s_in, s.ev_out, 0));  // its buffers drained
+        }
+        std::memcpy(s.h_lens, l32 + c0, sizeof(uint32_t) * nc);
+        std::memcpy(s.h_offs, offsets + c0, sizeof(uint64_t) * nc);
+        if (span[b]) HIP_TRY(hipMemcpyAsync(s.d_dense, in + lo[b], span[b], hipMemcpyHostToDevice, p->s_in));
+        HIP_TRY(hipMemcpyAsync(s.d_lens, s.h_lens, sizeof(uint32_t) * nc, hipMemcpyHostToDevice, p->s_in));
+        HIP_TRY(hipMemcpyAsync(s.d_offs, s.h_offs, sizeof(uint64_t) * nc, hipMemcpyHostToDevice, p->s_in));
+        HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
+        HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
+        k_expand_based<<<grid_for(nc * 64), kBlock, 0, sc>>>(s.d_dense, s.d_offs, lo[b], s.d_lens, nc, s.d_slots,
+                                                              slot_cap);
+        HIP_TRY(hipGetLastError());
+        if ((rc = launch_decode<Sym>(gt, s.d_slots, nullptr, slot_cap, s.d_lens, nb, chunk_len, gen_kind, s.d_syms,
+                                     p->d_status, sc)))
+            return rc;
+        HIP_TRY(hipEventRecord(s.ev_comp, sc));
+        HIP_TRY(hipStreamWaitEvent(p->s_out, s.ev_comp, 0));
+        HIP_TRY(hipMemcpyAsync(dst + n0 * w, s.d_syms, nb * w, hipMemcpyDeviceToHost, p->s_out));
+        HIP_TRY(hipEventRecord(s.ev_out, p->s_out));
+        s.used = true;
+    }
+    HIP_TRY(hipStreamSynchronize(p->s_out));
+    HIP_TRY(hipStreamSynchronize(p->s_comp2));
+    int st = 0;
+    if ((rc = ans_dev_status(gt->g, p->d_status, gt->g->stream, &st))) return rc;
+    return st;
+}
+
+// ---- page-locked host buffers: the GPU moves the bytes itself (no runtime copy calls)
+//
+// Page-locked host memory is mapped into the GPU's address space, so copy kernels can read
+// and write it across PCIe directly (tools/pinned_probe.hip: ~41 GB/s each way with both
+// directions in flight, ~55 GB/s alone).  The per-batch work then needs no host
+// synchronisation at all: batch offsets are scanned and carried on the device, and the
+// copy-out kernel reads its destination offset and size from device memory.
+
+// Copy engine for page-locked buffers: the runtime's copies (default: measured faster,
+// DESIGN.md §8) or these kernels (ANS_PIPE_COPY=kernel, the A/B switch behind that table).
+bool pipe_kernel_copies() {
+    const char* e = getenv("ANS_PIPE_COPY");  // read per call (tests switch it)
+    return e && std::strcmp(e, "kernel") == 0;
+}
+
+// Device-visible address of a page-locked host pointer (nullptr for pageable memory).
+uint8_t* mapped_ptr(const void* p) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    return static_cast<uint8_t*>(a.devicePointer);
+}
+
+constexpr unsigned kXferGrid = 128;  // workgroups per copy kernel (probe: 64-256 saturate PCIe)
+
+// dst[0..bytes) = src[0..bytes) between device memory and mapped host memory; 16-byte
+// accesses when dst and src agree mod 16 (the pipeline arranges that), bytes otherwise.
+__device__ __forceinline__ void xfer_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t bytes) {
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t nth = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    if (((reinterpret_cast<uintptr_t>(dst) ^ reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        const uint64_t head = std::min<uint64_t>(bytes, (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15);
+        if (tid < head) dst[tid] = src[tid];
+        const uint64_t n16 = (bytes - head) / 16;
+        uint4* d = reinterpret_cast<uint4*>(dst + head);
+        const uint4* s = reinterpret_cast<const uint4*>(src + head);
+        for (uint64_t i = tid; i < n16; i += nth) d[i] = s[i];
+        const uint64_t done = head + 16 * n16;
+        if (tid < bytes - done) dst[done + tid] = src[done + tid];
+    } else {
+        for (uint64_t i = tid; i < bytes; i += nth) dst[i] = src[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_xfer(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t bytes) {
+    xfer_bytes(dst, src, bytes);
+}
+
+// Batch scan for the mapped encoder: like k_scan_lens, plus the running container offset.
+// base = *acc (the bytes of all earlier batches), *acc += total; offs[n] = total,
+// offs[n+1] = base; each chunk's absolute offset and length go to the host arrays.
+__global__ __launch_bounds__(1024) void k_scan_carry(const uint32_t* __restrict__ lens, uint64_t n,
+                                                     uint64_t* __restrict__ offs, uint64_t* __restrict__ acc,
+                                                     uint64_t* __restrict__ h_offs, uint64_t* __restrict__ h_lens) {
+    __shared__ uint64_t part[1024];
+    __shared__ uint64_t base;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) base = *acc;
+    const uint64_t per = (n + 1023) / 1024, b = t * per, e = b + per < n ? b + per : n;
+    uint64_t sum = 0;
+    for (uint64_t i = b; i < e; ++i) sum += lens[i];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint64_t i = b; i < e; ++i) {
+        offs[i] = run;
+        run += lens[i];
+    }
+    if (t == 1023) {
+        offs[n] = part[1023];
+        offs[n + 1] = base;
+        *acc = base + part[1023];
+    }
+    __syncthreads();
+    for (uint64_t i = t; i < n; i += 1024) {  // coalesced writes across PCIe
+        h_offs[i] = base + offs[i];
+        h_lens[i] = lens[i];
+    }
+}
+
+// Slots -> dense bytes at dense + sh + offs[c], sh = (out + base) & 15 so that the copy-out
+// kernel's source and destination agree mod 16.
+__global__ __launch_bounds__(kBlock) void k_compact_at(const uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                       const uint32_t* __restrict__ lens,
+                                                       const uint64_t* __restrict__ offs, uint64_t nchunks,
+                                                       uintptr_t out_addr, uint8_t* __restrict__ dense) {
+    const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
+    const uint64_t sh = (out_addr + offs[nchunks + 1]) & 15;
+    const uint8_t* s = slots + c * slot_cap;
+    uint8_t* d = dense + sh + offs[c];
+    wave_copy(d, s, lens[c], lane);
+}
+
+// Copy-out of one encoded batch to out + base (size and base from the scan); a batch that
+// would overrun out_cap is not copied and flags ANS_E_LEN (coding continues, so the exact
+// total is still known).
+__global__ __launch_bounds__(256) void k_xfer_out(uint8_t* __restrict__ out, uint64_t out_cap,
+                                                  const uint8_t* __restrict__ dense, const uint64_t* __restrict__ offs,
+                                                  uint64_t nchunks, uint32_t* __restrict__ status) {
+    const uint64_t total = offs[nchunks], base = offs[nchunks + 1];
+    if (base + total > out_cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(status, 1u << ANS_E_LEN);
+        return;
+    }
+    const uint64_t sh = (reinterpret_cast<uintptr_t>(out) + base) & 15;
+    xfer_bytes(out + base, dense + sh, total);
+}
+
+// Dense batch bytes (at dense + sh, sh = (in + lo) & 15) -> slots; the chunk offsets and
+// lengths are read from the mapped host staging, lengths also land in d_lens for the decoder.
+__global__ __launch_bounds__(kBlock) void k_expand_mapped(const uint8_t* __restrict__ dense, uint64_t sh, uint64_t lo,
+                                                          const uint64_t* __restrict__ h_offs,
+                                                          const uint64_t* __restrict__ h_lens, uint64_t nchunks,
+                                                          uint32_t* __restrict__ d_lens, uint8_t* __restrict__ slots,
+                                                          uint64_t slot_cap) {
+    const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
+    const uint64_t off = h_offs[c];
+    const uint32_t len = static_cast<uint32_t>(h_lens[c]);
+    if (lane == 0) d_lens[c] = len;
+    const uint8_t* s = dense + sh + (off - lo);
+    uint8_t* d = slots + c * slot_cap;
+    wave_copy(d, s, len, lane);
+}
+
+// Host staging (mapped) for 2 x u64 per chunk of a whole call, and the device carry word.
+int pipe_meta(HostPipe* p, uint64_t nchunks) {
+    if (!p->d_acc) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_acc), 16));
+    if (!p->ev_scan) HIP_TRY(hipEventCreateWithFlags(&p->ev_scan, hipEventDisableTiming));
+    if (nchunks > p->cap_meta) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (p->h_meta) (void)hipHostFree(p->h_meta);
+        p->h_meta = nullptr;
+        p->cap_meta = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p->h_meta), 2 * sizeof(uint64_t) * nchunks + 16));
+        p->cap_meta = nchunks;
+    }
+    return ANS_OK;
+}
+
+// Encode with page-locked symbols and container.  Batch b: symbols in (k_xfer on s_in) ->
+// encode, carried scan, compaction (compute stream b & 1) -> container bytes out
+// (k_xfer_out on s_out).  The host only waits at the end.
+template <typename Sym>
+int pipe_encode_mapped(ans_gpu_table* gt, const uint8_t* syms_dev, uint64_t n, uint64_t chunk_len, uint8_t* out_dev,
+                       uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+    constexpr uint64_t w = sizeof(Sym);
+    const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    uint64_t slot_cap = 0;
+    ans_gpu_slot_capacity(gt, chunk_len, &slot_cap);
+    const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
+    HostPipe* p = nullptr;
+    int rc = pipe_get(gt->g, B * chunk_len * w, B * slot_cap, out_dev ? B * slot_cap + 16 : 0, B + 1, &p);
+    if (rc || (rc = pipe_meta(p, nchunks))) return rc;
+    uint64_t* h_offs = p->h_meta;
+    uint64_t* h_lens = p->h_meta + nchunks;
+    const hipStream_t s0 = gt->g->stream;
+    HIP_TRY(hipMemsetAsync(p->d_status, 0, sizeof(uint32_t), s0));
+    HIP_TRY(hipMemsetAsync(p->d_acc, 0, sizeof(uint64_t), s0));
+    HIP_TRY(hipStreamSynchronize(s0));
+    const uint64_t nbatch = (nchunks + B - 1) / B;
+    for (uint64_t b = 0; b < nbatch; ++b) {
+        PipeSlot& s = p->slot[b % kPipeDepth];
+        const hipStream_t sc = (b & 1) ? p->s_comp2 : s0;
+        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
+        const uint64_t nb = std::min(n - n0, nc * chunk_len);
+        if (s.used) HIP_TRY(hipStreamWaitEvent(p->s_in, s.ev_comp, 0));  // symbols of batch b - depth consumed
+        k_xfer<<<kXferGrid, 256, 0, p->s_in>>>(static_cast<uint8_t*>(s.d_syms), syms_dev + n0 * w, nb * w);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
+        HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
+        if (s.used) HIP_TRY(hipStreamWaitEvent(sc, s.ev_out, 0));  // dense bytes of batch b - depth copied out
+        if ((rc = launch_encode<Sym>(gt, s.d_syms, nb, chunk_len, s.d_slots, slot_cap, s.d_lens, p->d_status, sc)))
+            return rc;
+        if (b > 0) HIP_TRY(hipStreamWaitEvent(sc, p->ev_scan, 0));  // the carry runs in batch order
+        k_scan_carry<<<1, 1024, 0, sc>>>(s.d_lens, nc, s.d_offs, p->d_acc, h_offs + c0, h_lens + c0);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(p->ev_scan, sc));
+        if (out_dev) {
+            k_compact_at<<<grid_for(nc * 64), kBlock, 0, sc>>>(s.d_slots, slot_cap, s.d_lens, s.d_offs, nc,
+                                                               reinterpret_cast<uintptr_t>(out_dev), s.d_dense);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipEventRecord(s.ev_comp, sc));
+        HIP_TRY(hipStreamWaitEvent(p->s_out, s.ev_comp, 0));
+        if (out_dev) {
+            k_xfer_out<<<kXferGrid, 256, 0, p->s_out>>>(out_dev, out_cap, s.d_dense, s.d_offs, nc, p->d_status);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipEventRecord(s.ev_out, p->s_out));
+        s.used = true;
+    }
+    HIP_TRY(hipStreamSynchronize(p->s_out));
+    HIP_TRY(hipStreamSynchronize(p->s_comp2));
+    HIP_TRY(hipStreamSynchronize(s0));
+    uint32_t bits = 0;
+    uint64_t acc = 0;
+    HIP_TRY(hipMemcpy(&bits, p->d_status, sizeof(bits), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&acc, p->d_acc, sizeof(acc), hipMemcpyDeviceToHost));
+    const int st = lowest_status(bits & ~(1u << ANS_E_LEN));
+    if (st) return st;
+    *total = acc;
+    if (!out_dev) return ANS_OK;
+    std::memcpy(offsets, h_offs, sizeof(uint64_t) * nchunks);
+    std::memcpy(lens, h_lens, sizeof(uint64_t) * nchunks);
+    return (bits & (1u << ANS_E_LEN)) ? ANS_E_LEN : ANS_OK;
+}
+
+// Decode from a page-locked container into page-locked symbols.  Batch b: its byte span in
+// (k_xfer on s_in) -> expansion (offsets and lengths read from the mapped staging) and
+// decode (compute stream b & 1) -> symbols out (k_xfer on s_out).  No host waits in the loop.
+template <typename Sym>
+int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t* offsets, const uint32_t* l32,
+                       uint64_t slot_cap, uint64_t n, uint64_t chunk_len, int gen_kind, uint8_t* out_dev) {
+    constexpr uint64_t w = sizeof(Sym);
+    const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
+    const uint64_t nbatch = (nchunks + B - 1) / B;
+    std::vector<uint64_t> lo(nbatch), span(nbatch);
+    uint64_t max_span = 0;
+    for (uint64_t b = 0; b < nbatch; ++b) {
+        const uint64_t c0 = b * B, c1 = std::min(nchunks, c0 + B);
+        uint64_t l = ~0ull, h = 0;
+        for (uint64_t j = c0; j < c1; ++j) {
+            l = std::min(l, offsets[j]);
+            h = std::max(h, offsets[j] + l32[j]);
+        }
+        lo[b] = l;
+        span[b] = h - l;
+        max_span = std::max(max_span, span[b]);
+    }
+    if (max_span > 2 * B * slot_cap) return kPipeScattered;
+    HostPipe* p = nullptr;
+    int rc = pipe_get(gt->g, B * chunk_len * w, B * slot_cap, max_span + 16, B + 1, &p);
+    if (rc || (rc = pipe_meta(p, nchunks))) return rc;
+    uint64_t* h_offs = p->h_meta;
+    uint64_t* h_lens = p->h_meta + nchunks;
+    std::memcpy(h_offs, offsets, sizeof(uint64_t) * nchunks);
+    for (uint64_t j = 0; j < nchunks; ++j) h_lens[j] = l32[j];
+    const hipStream_t s0 = gt->g->stream;
+    HIP_TRY(hipMemsetAsync(p->d_status, 0, sizeof(uint32_t), s0));
+    HIP_TRY(hipStreamSynchronize(s0));
+    for (uint64_t b = 0; b < nbatch; ++b) {
+        PipeSlot& s = p->slot[b % kPipeDepth];
+        const hipStream_t sc = (b & 1) ? p->s_comp2 : s0;
+        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
+        const uint64_t nb = std::min(n - n0, nc * chunk_len);
+        const uint64_t sh = reinterpret_cast<uintptr_t>(in_dev + lo[b]) & 15;
+        if (s.used) HIP_TRY(hipStreamWaitEvent(p->s_in, s.ev_out, 0));  // batch b - depth drained
+        k_xfer<<<kXferGrid, 256, 0, p->s_in>>>(s.d_dense + sh, in_dev + lo[b], span[b]);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
+        HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
+        k_expand_mapped<<<grid_for(nc * 64), kBlock, 0, sc>>>(s.d_dense, sh, lo[b], h_offs + c0, h_lens + c0, nc,
+                                                              s.d_lens, s.d_slots, slot_cap);
+        HIP_TRY(hipGetLastError());
+        if ((rc = launch_decode<Sym>(gt, s.d_slots, nullptr, slot_cap, s.d_lens, nb, chunk_len, gen_kind, s.d_syms,
+                                     p->d_status, sc)))
+            return rc;
+        HIP_TRY(hipEventRecord(s.ev_comp, sc));
+        HIP_TRY(hipStreamWaitEvent(p->s_out, s.ev_comp, 0));
+        k_xfer<<<kXferGrid, 256, 0, p->s_out>>>(out_dev + n0 * w, static_cast<const uint8_t*>(s.d_syms), nb * w);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(s.ev_out, p->s_out));
+        s.used = true;
+    }
+    HIP_TRY(hipStreamSynchronize(p->s_out));
+    HIP_TRY(hipStreamSynchronize(p->s_comp2));
+    int st = 0;
+    if ((rc = ans_dev_status(gt->g, p->d_status, s0, &st))) return rc;
+    return st;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI (GPU part)
@@ -569,7 +1203,7 @@ int ans_gpu_create(int device, ans_gpu** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return ANS_E_DEVICE;
     HIP_TRY(hipSetDevice(device));
-    auto* g = new (std::nothrow) ans_gpu{device, nullptr};
+    auto* g = new (std::nothrow) ans_gpu{device, nullptr, nullptr, 0};
     if (!g) return ANS_E_ALLOC;
     if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
         delete g;
@@ -579,9 +1213,30 @@ int ans_gpu_create(int device, ans_gpu** out) {
     return ANS_OK;
 }
 
+int ans_host_alloc(size_t bytes, void** out) {
+    if (!out) return ANS_E_ARG;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return ANS_E_ALLOC;
+    }
+    return ANS_OK;
+}
+
+void ans_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int ans_gpu_set_batch_bytes(ans_gpu* g, uint64_t batch_bytes) {
+    if (!g) return ANS_E_ARG;
+    g->batch_bytes = batch_bytes;
+    return ANS_OK;
+}
+
 void ans_gpu_free(ans_gpu* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
+    pipe_free(g);
     (void)hipStreamDestroy(g->stream);
     delete g;
 }
@@ -730,49 +1385,24 @@ int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, ui
     if (n && !syms) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (out && nchunks && (!offsets || !lens)) return ANS_E_ARG;
-    uint64_t slot_cap = 0;
-    ans_gpu_slot_capacity(gt, chunk_len, &slot_cap);
-    HIP_TRY(hipSetDevice(gt->g->device));
-    const hipStream_t s = gt->g->stream;
-    DevBuf d_syms, d_slots, d_lens, d_status, d_offsets, d_out;
-    HIP_TRY(d_syms.alloc(n * sym_bytes));
-    HIP_TRY(d_slots.alloc(nchunks * slot_cap));
-    HIP_TRY(d_lens.alloc(nchunks * sizeof(uint32_t)));
-    HIP_TRY(d_status.alloc(sizeof(uint32_t)));
-    HIP_TRY(hipMemcpyAsync(d_syms.p, syms, n * sym_bytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(d_status.p, 0, sizeof(uint32_t), s));
-    int rc = ans_dev_encode_chunks(gt, d_syms.p, sym_bytes, n, chunk_len, static_cast<uint8_t*>(d_slots.p), slot_cap,
-                                   static_cast<uint32_t*>(d_lens.p), static_cast<uint32_t*>(d_status.p), s);
-    if (rc) return rc;
-    int st = 0;
-    rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st);
-    if (rc) return rc;
-    if (st) return st;
-    std::vector<uint32_t> hl(nchunks);
-    HIP_TRY(hipMemcpy(hl.data(), d_lens.p, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    std::vector<uint64_t> off(nchunks);
-    uint64_t acc = 0;
-    for (uint64_t j = 0; j < nchunks; ++j) {
-        off[j] = acc;
-        acc += hl[j];
-    }
-    *total = acc;
-    if (!out) return ANS_OK;
-    if (out_cap < acc) return ANS_E_LEN;
-    for (uint64_t j = 0; j < nchunks; ++j) {
-        offsets[j] = off[j];
-        lens[j] = hl[j];
-    }
+    *total = 0;
     if (nchunks == 0) return ANS_OK;
-    HIP_TRY(d_offsets.alloc(nchunks * sizeof(uint64_t)));
-    HIP_TRY(d_out.alloc(acc));
-    HIP_TRY(hipMemcpyAsync(d_offsets.p, off.data(), nchunks * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    rc = ans_dev_compact(gt->g, static_cast<uint8_t*>(d_slots.p), slot_cap, static_cast<uint32_t*>(d_lens.p),
-                         static_cast<uint64_t*>(d_offsets.p), nchunks, static_cast<uint8_t*>(d_out.p), s);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out, d_out.p, acc, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return ANS_OK;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    // page-locked symbols and container (or a size query): device-driven copies
+    uint8_t* syms_dev = pipe_kernel_copies() ? mapped_ptr(syms) : nullptr;
+    uint8_t* out_dev = out && syms_dev ? mapped_ptr(out) : nullptr;
+    if (syms_dev && (!out || out_dev)) {
+        switch (sym_bytes) {
+        case 1: return pipe_encode_mapped<uint8_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total);
+        case 2: return pipe_encode_mapped<uint16_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total);
+        default: return pipe_encode_mapped<uint32_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total);
+        }
+    }
+    switch (sym_bytes) {
+    case 1: return pipe_encode<uint8_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total);
+    case 2: return pipe_encode<uint16_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total);
+    default: return pipe_encode<uint32_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total);
+    }
 }
 
 int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
@@ -781,6 +1411,8 @@ int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len,
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks && (!in || !offsets || !lens || !out)) return ANS_E_ARG;
+    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;
+    if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
     std::vector<uint32_t> l32(nchunks);
     for (uint64_t j = 0; j < nchunks; ++j) {
         if (lens[j] > 0xffffffffull || offsets[j] > in_len || lens[j] > in_len - offsets[j]) return ANS_E_LEN;
@@ -794,6 +1426,26 @@ int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len,
     for (uint64_t j = 0; j < nchunks; ++j) max_len = std::max<uint64_t>(max_len, l32[j]);
     slot_cap = std::max<uint64_t>(slot_cap, (max_len + 64 + 127) & ~uint64_t(127));
     HIP_TRY(hipSetDevice(gt->g->device));
+    if (nchunks) {  // dense containers (the encoder's output) take the pipelined path
+        int rc = kPipeScattered;
+        uint8_t* in_dev = pipe_kernel_copies() ? mapped_ptr(in) : nullptr;
+        uint8_t* out_dev = in_dev ? mapped_ptr(out) : nullptr;
+        if (in_dev && out_dev) {
+            switch (sym_bytes) {
+            case 1: rc = pipe_decode_mapped<uint8_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev); break;
+            case 2: rc = pipe_decode_mapped<uint16_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev); break;
+            default: rc = pipe_decode_mapped<uint32_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev); break;
+            }
+            if (rc != kPipeScattered) return rc;
+        }
+        switch (sym_bytes) {
+        case 1: rc = pipe_decode<uint8_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out); break;
+        case 2: rc = pipe_decode<uint16_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out); break;
+        default: rc = pipe_decode<uint32_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out); break;
+        }
+        if (rc != kPipeScattered) return rc;
+    }
+    // streams scattered over the buffer: one upload of the whole input
     const hipStream_t s = gt->g->stream;
     DevBuf d_in, d_off, d_lens, d_status, d_out, d_slots;
     HIP_TRY(d_in.alloc(in_len + 16));

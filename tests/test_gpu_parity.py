@@ -272,3 +272,111 @@ def test_dense_and_slot_layouts_decode_alike(gpu, sym_bytes):
     finally:
         torch.cuda.synchronize()
         torch.cuda.set_stream(torch.cuda.default_stream())
+
+
+# ---------------------------------------------------------------- host-buffer pipeline
+@pytest.mark.parametrize("sym_bytes,batch_bytes", [(1, 1 << 20), (2, 3 << 19), (1, 4096 * 7)])
+def test_host_pipeline_many_batches(sym_bytes, batch_bytes):
+    """ans_gpu_encode_chunks / ans_gpu_decode_chunks split the call into batches that
+    overlap copies and kernels; the container must equal the oracle's whatever the batch
+    size, including a ragged last chunk in the last batch."""
+    g = A.Gpu(0)
+    g.set_batch_bytes(batch_bytes)
+    masses = A.c3_masses()
+    gt = A.GpuTable(g, A.Categorical(masses))
+    dtype = {1: np.uint8, 2: np.uint16}[sym_bytes]
+    n, L = 1000 * 4096 + 777, 4096
+    syms = orc.gen_iid(masses, 11, 0, n).astype(dtype)
+    data, offsets, lens = gt.encode_chunks(syms, L)
+    odata, ooffsets, olens = orc.encode_chunks(masses, syms.astype(np.uint32), L)
+    assert np.array_equal(lens, olens) and np.array_equal(offsets, ooffsets)
+    assert data.tobytes() == odata.tobytes()
+    back = gt.decode_chunks(data, offsets, lens, n, L, dtype)
+    assert np.array_equal(back, syms)
+    # the same context again (workspace reuse), and a size query with no output buffer
+    data2, _, _ = gt.encode_chunks(syms, L)
+    assert data2.tobytes() == odata.tobytes()
+    total = A.u64(0)
+    rc = A.lib().ans_gpu_encode_chunks(gt.h, A._np_ptr(syms), sym_bytes, n, L, None, 0, None, None,
+                                       A.ctypes.byref(total))
+    assert rc == 0 and total.value == len(odata)
+
+
+def test_host_pipeline_errors_and_scattered_container():
+    g = A.Gpu(0)
+    g.set_batch_bytes(1 << 18)
+    masses = A.c3_masses()
+    gt = A.GpuTable(g, A.Categorical(masses))
+    n, L = 300 * 4096, 4096
+    syms = orc.gen_iid(masses, 5, 0, n).astype(np.uint8)
+    data, offsets, lens = gt.encode_chunks(syms, L)
+    # output buffer one byte short: ANS_E_LEN, with the exact total still reported
+    out = np.empty(len(data) - 1, np.uint8)
+    offs = np.zeros(len(lens), np.uint64)
+    ls = np.zeros(len(lens), np.uint64)
+    total = A.u64(0)
+    rc = A.lib().ans_gpu_encode_chunks(gt.h, A._np_ptr(syms), 1, n, L, A._np_ptr(out), len(out), A._np_ptr(offs),
+                                       A._np_ptr(ls), A.ctypes.byref(total))
+    assert rc == A.ANS_E_LEN and total.value == len(data)
+    # streams stored far apart and out of order: the whole-buffer path decodes them
+    gap = 10_000
+    order = np.arange(len(lens))[::-1]
+    scattered = np.zeros(int(lens.sum()) + gap * len(lens), np.uint8)
+    soff = np.zeros(len(lens), np.uint64)
+    pos = 0
+    for j in order:
+        soff[j] = pos
+        scattered[pos:pos + int(lens[j])] = data[int(offsets[j]):int(offsets[j] + lens[j])]
+        pos += int(lens[j]) + gap
+    back = gt.decode_chunks(scattered, soff, lens, n, L, np.uint8)
+    assert np.array_equal(back, syms)
+    # a corrupted stream in a middle batch is reported
+    bad = data.copy()
+    bad[int(offsets[150]) + 3] ^= 0x33
+    with pytest.raises(A.AnsError) as e:
+        gt.decode_chunks(bad, offsets, lens, n, L, np.uint8)
+    assert e.value.code == A.ANS_E_MISMATCH
+
+
+@pytest.mark.parametrize("engine", ["runtime", "kernel"])
+@pytest.mark.parametrize("sym_bytes,batch_bytes,skew", [(1, 1 << 20, 0), (2, 3 << 19, 0), (1, 4096 * 7, 3),
+                                                       (2, 1 << 20, 5)])
+def test_host_pipeline_page_locked(sym_bytes, batch_bytes, skew, engine, monkeypatch):
+    """Page-locked (ans_host_alloc) buffers: asynchronous runtime copies (default), or with
+    ANS_PIPE_COPY=kernel the device-driven path (copy kernels over PCIe, the container offset
+    carried on the device).  `skew` shifts every buffer off 16-byte alignment."""
+    monkeypatch.setenv("ANS_PIPE_COPY", engine)
+    g = A.Gpu(0)
+    g.set_batch_bytes(batch_bytes)
+    masses = A.c3_masses()
+    gt = A.GpuTable(g, A.Categorical(masses))
+    dtype = {1: np.uint8, 2: np.uint16}[sym_bytes]
+    n, L = 900 * 4096 + 1001, 4096
+    ref = orc.gen_iid(masses, 13, 0, n).astype(dtype)
+    syms = A.pinned_empty(n + skew, dtype)[skew:]
+    syms[:] = ref
+    nchunks = -(-n // L)
+    cap = nchunks * gt.slot_capacity(L)
+    out = A.pinned_empty(cap + skew, np.uint8)[skew:]
+    offsets = np.zeros(nchunks, np.uint64)
+    lens = np.zeros(nchunks, np.uint64)
+    total = A.u64(0)
+    A._check(A.lib().ans_gpu_encode_chunks(gt.h, A._np_ptr(syms), sym_bytes, n, L, A._np_ptr(out), cap,
+                                           A._np_ptr(offsets), A._np_ptr(lens), A.ctypes.byref(total)), "encode")
+    odata, ooffsets, olens = orc.encode_chunks(masses, ref.astype(np.uint32), L)
+    assert total.value == len(odata)
+    assert np.array_equal(lens, olens) and np.array_equal(offsets, ooffsets)
+    assert out[:total.value].tobytes() == odata.tobytes()
+    back = A.pinned_empty(n + skew, dtype)[skew:]
+    A._check(A.lib().ans_gpu_decode_chunks(gt.h, A._np_ptr(out), total.value, A._np_ptr(offsets), A._np_ptr(lens),
+                                           n, L, A.GEN_ZEROS, A._np_ptr(back), sym_bytes), "decode")
+    assert np.array_equal(back, ref)
+    # a too-small page-locked output: ANS_E_LEN with the exact total
+    rc = A.lib().ans_gpu_encode_chunks(gt.h, A._np_ptr(syms), sym_bytes, n, L, A._np_ptr(out), total.value - 1,
+                                       A._np_ptr(offsets), A._np_ptr(lens), A.ctypes.byref(total))
+    assert rc == A.ANS_E_LEN and total.value == len(odata)
+    # corruption in a middle batch is reported through the mapped path too
+    out[int(ooffsets[nchunks // 2]) + 2] ^= 0x41
+    rc = A.lib().ans_gpu_decode_chunks(gt.h, A._np_ptr(out), len(odata), A._np_ptr(offsets), A._np_ptr(lens),
+                                       n, L, A.GEN_ZEROS, A._np_ptr(back), sym_bytes)
+    assert rc == A.ANS_E_MISMATCH
