@@ -164,8 +164,41 @@ int ans_dev_gen_iid(ans_gpu_table *gt, uint64_t seed, uint64_t start, uint64_t n
 /* Compacts slot streams into a dense buffer: d_out[d_offsets[j] ..] = slot j. */
 int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const uint32_t *d_lens,
                     const uint64_t *d_offsets, uint64_t nchunks, uint8_t *d_out, void *stream);
+/* The inverse of ans_dev_compact: dense-container streams into the slot layout (which the
+ * fast decode kernels read). */
+int ans_dev_expand(ans_gpu *g, const uint8_t *d_in, const uint64_t *d_offsets, const uint32_t *d_lens,
+                   uint64_t nchunks, uint8_t *d_slots, uint64_t slot_cap, void *stream);
 /* Synchronises `stream` and maps the device status word to the lowest set status. */
 int ans_dev_status(ans_gpu *g, const uint32_t *d_status, void *stream, int *status);
+
+/* ======================================================================
+ * (5) Graph models' bulk-IID caller — DenseSetIID<EdgeIndex, AllEdgeIndices> with an
+ *     IID<Bernoulli> (ErdosRenyi, src/graph_codec.rs:105-205).  Edges are uint32 pairs
+ *     (i, j) (EdgeIndex, src/graph.rs:17), num_nodes < 2^32.  The alphabet is the reference's
+ *     AllEdgeIndices order (src/graph_codec.rs:187-199): self-loops (i,i) first when `loops`,
+ *     then for j in 0..n, i in 0..j: (i,j), followed by (j,i) when `directed`.  An edge outside
+ *     the alphabet (undirected (j,i) with j > i, a loop without `loops`, a node >= n) is
+ *     ANS_E_SYMBOL, where DenseSetIID::dense panics (src/graph_codec.rs:137).
+ * ====================================================================== */
+/* num_all_edge_indices  src/graph_codec.rs:203-205 */
+int ans_edge_alphabet_len(uint64_t num_nodes, int directed, int loops, uint64_t *len);
+/* DenseSetIID::dense  src/graph_codec.rs:133-138: d_dense[slot(edge)] = 1, others 0 (u8) */
+int ans_dev_edges_to_dense(ans_gpu *g, uint64_t num_nodes, int directed, int loops, const uint32_t *d_edges,
+                           uint64_t num_edges, uint8_t *d_dense, uint32_t *d_status, void *stream);
+/* the filter of DenseSetIID::pop  src/graph_codec.rs:117-120: the set slots' edges in
+ * alphabet order into d_edges (at most cap; ANS_E_LEN in *d_status beyond), count in *d_count */
+int ans_dev_dense_to_edges(ans_gpu *g, uint64_t num_nodes, int directed, int loops, const uint8_t *d_dense,
+                           uint32_t *d_edges, uint64_t cap, uint64_t *d_count, uint32_t *d_status, void *stream);
+/* ErdosRenyi push / pop (src/graph_codec.rs:152-155), chunked like section (4): the dense
+ * vector over the alphabet, coded with a Bernoulli table (ans_table_create_bernoulli; the
+ * reference's Bernoulli::new(total_edges, total_possible_edges), src/benchmark.rs:556);
+ * chunk j is one reference message over slots [j*chunk_len, (j+1)*chunk_len). */
+int ans_gpu_dense_set_encode(ans_gpu_table *gt, uint64_t num_nodes, int directed, int loops, const uint32_t *edges,
+                             uint64_t num_edges, uint64_t chunk_len, uint8_t *out, uint64_t out_cap,
+                             uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_dense_set_decode(ans_gpu_table *gt, uint64_t num_nodes, int directed, int loops, const uint8_t *in,
+                             uint64_t in_len, const uint64_t *offsets, const uint64_t *lens, uint64_t chunk_len,
+                             uint32_t *edges, uint64_t cap, uint64_t *num_edges);
 
 #ifdef __cplusplus
 }

@@ -225,3 +225,43 @@ def gen_iid(masses, seed, start, n):
 
 def splitmix64(x):
     return lib().orc_splitmix64(x)
+
+
+# ---------------------------------------------------------------- graph models (src/graph_codec.rs)
+def all_edge_indices(num_nodes, directed, loops):
+    """AllEdgeIndices::into_iter (src/graph_codec.rs:187-199), literally: the loops first,
+    then `(0..n).flat_map(|j| (0..j).map(|i| (i, j)))`, each followed by (j, i) if directed."""
+    out = [(i, i) for i in range(num_nodes)] if loops else []
+    for j in range(num_nodes):
+        for i in range(j):
+            out.append((i, j))
+            if directed:
+                out.append((j, i))
+    return out
+
+
+def edge_slots(edges, num_nodes, directed, loops):
+    """Vectorised position of each edge in all_edge_indices order (-1 outside the alphabet);
+    checked against the literal enumeration in tests/test_oracle.py."""
+    e = np.asarray(edges, dtype=np.int64).reshape(-1, 2)
+    i, j = e[:, 0], e[:, 1]
+    base = num_nodes if loops else 0
+    a, b = np.minimum(i, j), np.maximum(i, j)
+    pair = b * (b - 1) // 2 + a
+    if directed:
+        slot = base + 2 * pair + (i > j)
+    else:
+        slot = np.where(i < j, base + pair, -1)
+    slot = np.where(i == j, i if loops else -1, slot)
+    return np.where((i < num_nodes) & (j < num_nodes) & (i >= 0) & (j >= 0), slot, -1)
+
+
+def dense_set(edges, num_nodes, directed, loops):
+    """DenseSetIID::dense (src/graph_codec.rs:133-138) as a u8 indicator vector."""
+    n = (num_nodes if loops else 0) + (num_nodes * num_nodes - num_nodes) // (1 if directed else 2)
+    s = edge_slots(edges, num_nodes, directed, loops)
+    if (s < 0).any():
+        raise ValueError("edge outside the alphabet (the reference panics, src/graph_codec.rs:137)")
+    d = np.zeros(n, np.uint8)
+    d[s] = 1
+    return d

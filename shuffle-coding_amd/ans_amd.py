@@ -81,6 +81,12 @@ SIGNATURES = {
     "ans_dev_gen_iid": (ci, [vp, u64, u64, u64, vp, ci, vp]),
     "ans_dev_compact": (ci, [vp, vp, u64, vp, vp, u64, vp, vp]),
     "ans_dev_status": (ci, [vp, vp, vp, ctypes.POINTER(ci)]),
+    "ans_dev_expand": (ci, [vp, vp, vp, vp, u64, vp, u64, vp]),
+    "ans_edge_alphabet_len": (ci, [u64, ci, ci, u64p]),
+    "ans_dev_edges_to_dense": (ci, [vp, u64, ci, ci, vp, u64, vp, vp, vp]),
+    "ans_dev_dense_to_edges": (ci, [vp, u64, ci, ci, vp, vp, u64, vp, vp, vp]),
+    "ans_gpu_dense_set_encode": (ci, [vp, u64, ci, ci, vp, u64, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_dense_set_decode": (ci, [vp, u64, ci, ci, vp, u64, vp, vp, u64, vp, u64, u64p]),
 }
 
 _lib = None
@@ -414,19 +420,30 @@ class IID(Codec):  # src/codec.rs:405-443
         self.item = item
         self.len = length
 
+    def _table(self):
+        if isinstance(self.item, Categorical):
+            return self.item.table
+        if isinstance(self.item, Bernoulli):
+            return self.item.categorical.table
+        return None
+
     def push(self, m, x):
         assert len(x) == self.len
-        if isinstance(self.item, Categorical):
+        table = self._table()
+        if table is not None:
             s = np.ascontiguousarray(np.asarray(x, dtype=np.uint32))
-            _check(lib().ans_push_iid(m.h, self.item.table, _np_ptr(s), len(s)), "IID::push")
+            _check(lib().ans_push_iid(m.h, table, _np_ptr(s), len(s)), "IID::push")
             return
         for e in reversed(list(x)):
             self.item.push(m, e)
 
     def pop(self, m):
-        if isinstance(self.item, Categorical):
+        table = self._table()
+        if table is not None:
             out = np.zeros(max(self.len, 1), np.uint32)
-            _check(lib().ans_pop_iid(m.h, self.item.table, _np_ptr(out), self.len), "IID::pop")
+            _check(lib().ans_pop_iid(m.h, table, _np_ptr(out), self.len), "IID::pop")
+            if isinstance(self.item, Bernoulli):
+                return [bool(v) for v in out[:self.len]]
             return [int(v) for v in out[:self.len]]
         return [self.item.pop(m) for _ in range(self.len)]
 
@@ -604,6 +621,120 @@ class GpuTable:
     def dev_gen_iid(self, seed, start, n, d_syms, sym_bytes, stream=None):
         _check(lib().ans_dev_gen_iid(self.h, seed, start, n, _dptr(d_syms), sym_bytes, _sptr(stream)),
                "ans_dev_gen_iid")
+
+
+# ============================================================== graph models' bulk caller (section 5)
+class AllEdgeIndices:
+    """The edge alphabet of src/graph_codec.rs:176-205 in the reference's order: the
+    self-loops (i, i) first when allowed, then for j in 0..n, i in 0..j the pair (i, j),
+    followed by (j, i) when directed."""
+
+    def __init__(self, num_nodes, directed=False, loops=False):
+        self.num_nodes, self.directed, self.loops = int(num_nodes), bool(directed), bool(loops)
+
+    def __len__(self):  # num_all_edge_indices, src/graph_codec.rs:203-205
+        n = u64(0)
+        _check(lib().ans_edge_alphabet_len(self.num_nodes, int(self.directed), int(self.loops), ctypes.byref(n)),
+               "num_all_edge_indices")
+        return n.value
+
+    def __iter__(self):
+        n = self.num_nodes
+        if self.loops:
+            for i in range(n):
+                yield (i, i)
+        for j in range(n):
+            for i in range(j):
+                yield (i, j)
+                if self.directed:
+                    yield (j, i)
+
+
+class DenseSetIID(Codec):
+    """src/graph_codec.rs:104-139: a set over `alphabet` coded as IID<Bernoulli> of its
+    indicator vector, on ONE message (the reference's bitstream)."""
+
+    def __init__(self, contains, alphabet):
+        self.alphabet = alphabet
+        self.contains = IID(contains, len(alphabet))
+
+    def dense(self, x):  # src/graph_codec.rs:133-138
+        rest = set(map(tuple, x))
+        out = []
+        for a in self.alphabet:
+            out.append(a in rest)
+            rest.discard(a)
+        if rest:
+            raise AnsError(ANS_E_SYMBOL, "DenseSetIID::dense: element outside the alphabet")
+        return out
+
+    def push(self, m, x):
+        self.contains.push(m, self.dense(x))
+
+    def pop(self, m):
+        d = self.contains.pop(m)
+        return [a for a, b in zip(self.alphabet, d) if b]
+
+    def bits(self, x):
+        return self.contains.bits(self.dense(x))
+
+
+class ErdosRenyi(DenseSetIID):
+    """erdos_renyi_indices (src/graph_codec.rs:172-174): DenseSetIID over AllEdgeIndices."""
+
+    def __init__(self, edge, num_nodes, directed=False, loops=False):
+        super().__init__(edge, AllEdgeIndices(num_nodes, directed, loops))
+        self.loops = loops
+
+
+class GpuDenseSet:
+    """The ErdosRenyi edge set on the GPU (section 5 of the C ABI): the dense indicator
+    vector is built on the device, coded by the bulk chunk path with the Bernoulli table and
+    decoded back to the edge list in alphabet order.  Chunk j is one reference message over
+    alphabet slots [j*chunk_len, (j+1)*chunk_len)."""
+
+    def __init__(self, gpu, edge, num_nodes, directed=False, loops=False):
+        self.gpu = gpu
+        self.edge = edge
+        self.table = GpuTable(gpu, edge.categorical)
+        self.space = (int(num_nodes), int(bool(directed)), int(bool(loops)))
+
+    def alphabet_len(self):
+        return len(AllEdgeIndices(*self.space))
+
+    def encode(self, edges, chunk_len):
+        """edges: (m, 2) integer array of (i, j).  Returns (bytes, offsets, lens)."""
+        e = np.ascontiguousarray(np.asarray(edges, dtype=np.uint32).reshape(-1, 2))
+        n = self.alphabet_len()
+        nchunks = -(-n // chunk_len)
+        out = np.empty(max(nchunks * self.table.slot_capacity(chunk_len), 1), np.uint8)
+        offsets = np.zeros(max(nchunks, 1), np.uint64)
+        lens = np.zeros(max(nchunks, 1), np.uint64)
+        total = u64(0)
+        _check(lib().ans_gpu_dense_set_encode(self.table.h, *self.space, _np_ptr(e), len(e), chunk_len, _np_ptr(out),
+                                              len(out), _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
+               "ans_gpu_dense_set_encode")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode(self, data, offsets, lens, chunk_len, cap=None):
+        data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+        offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        if cap is None:  # the expected edge count with room; a second pass if it is exceeded
+            cap = int(2 * self.edge.prob() * self.alphabet_len()) + 1024
+        cap = min(cap, self.alphabet_len())
+        for _ in range(2):
+            edges = np.zeros((max(cap, 1), 2), np.uint32)
+            count = u64(0)
+            rc = lib().ans_gpu_dense_set_decode(self.table.h, *self.space, _np_ptr(data) if data.size else None,
+                                                data.size, _np_ptr(offsets), _np_ptr(lens), chunk_len, _np_ptr(edges),
+                                                cap, ctypes.byref(count))
+            if rc == ANS_E_LEN and count.value > cap:
+                cap = count.value
+                continue
+            _check(rc, "ans_gpu_dense_set_decode")
+            return edges[:count.value]
+        raise AnsError(ANS_E_LEN, "ans_gpu_dense_set_decode")
 
 
 # ============================================================== synthetic tables (SURVEY.md §8d)

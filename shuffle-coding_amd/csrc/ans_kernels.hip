@@ -19,57 +19,7 @@
 #include <cstring>
 #include <vector>
 
-#include "ans_fast.hpp"
-#include "ans_table.hpp"
-
-using namespace shuffle_coding;
-
-// Host-buffer pipeline (ans_gpu_encode_chunks / ans_gpu_decode_chunks): batches of chunks
-// flow through kPipeDepth workspace slots, so that the H2D copy of batch b+1, the kernels of
-// batch b and the D2H copy of batch b-1 overlap.  Kernels alternate between
-// two compute streams (the context's and s_comp2): a batch's kernels occupy few CUs for about
-// one chain latency (~1 ms for 4096-symbol chunks), so consecutive batches must overlap too.
-// Four streams in all, the per-process hardware queue count.  The workspace persists in the
-// context and grows on demand.
-constexpr int kPipeDepth = 3;
-struct PipeSlot {
-    void* d_syms = nullptr;     // batch symbols
-    uint8_t* d_slots = nullptr; // batch streams in the slot layout
-    uint8_t* d_dense = nullptr; // batch streams, dense (encode output / decode input)
-    uint32_t* d_lens = nullptr;
-    uint64_t* d_offs = nullptr;  // batch offsets (+ total at [nchunks] after encode)
-    uint32_t* h_lens = nullptr;  // pinned staging
-    uint64_t* h_offs = nullptr;  // pinned staging
-    hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_meta = nullptr, ev_out = nullptr;
-    bool used = false;
-};
-struct HostPipe {
-    hipStream_t s_in = nullptr, s_out = nullptr, s_comp2 = nullptr;
-    PipeSlot slot[kPipeDepth];
-    uint32_t* d_status = nullptr;
-    size_t cap_syms = 0, cap_slots = 0, cap_dense = 0, cap_chunks = 0;  // per slot
-    // page-locked callers (device-driven copies): per-call chunk metadata and the carry
-    uint64_t* h_meta = nullptr;  // mapped host staging: offsets[nchunks], lens[nchunks]
-    size_t cap_meta = 0;
-    uint64_t* d_acc = nullptr;   // running container offset across batches
-    hipEvent_t ev_scan = nullptr;
-};
-
-struct ans_gpu {
-    int device;
-    hipStream_t stream;
-    HostPipe* pipe;
-    uint64_t batch_bytes;  // symbol bytes per pipeline batch (0 = default)
-};
-
-struct ans_gpu_table {
-    ans_gpu* g;
-    DevTable t;
-    void* d_mem;
-    uint32_t lds_bytes;  // 0 = table read from global memory (L2-resident)
-    FastTable ft;        // throughput path (ans_fast.hpp) when ft.usable
-    void* d_fast;
-};
+#include "ans_ctx.hpp"
 
 namespace {
 
@@ -327,8 +277,9 @@ __global__ __launch_bounds__(kBlock) void k_gen_iid(DevTable t, uint64_t seed, u
 }
 
 // One wave copies one stream: byte head until dst is dword-aligned, then aligned dword
-// stores funnelled from two source dwords (v_alignbyte), then the byte tail.  Reads up to 4
-// bytes past the source stream, which every caller's buffer has as slack.
+// stores funnelled from two source dwords (v_alignbyte), then the byte tail.  Source reads
+// are aligned dwords that each hold at least one byte of the stream (no over-read past the
+// dword holding its last byte).
 __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
                                           uint32_t lane) {
     const uint32_t head = min(len, (4u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst) & 3)) & 3u);
@@ -340,7 +291,7 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
     uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
     for (uint32_t i = lane; i < nd; i += 64) {
-        const uint32_t lo = s4[i], hi = s4[i + 1];
+        const uint32_t lo = s4[i], hi = sh ? s4[i + 1] : 0u;  // sh is wave-uniform
         d4[i] = __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
     if (lane < len - 4 * nd) dst[4 * nd + lane] = src[4 * nd + lane];
@@ -1203,7 +1154,7 @@ int ans_gpu_create(int device, ans_gpu** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return ANS_E_DEVICE;
     HIP_TRY(hipSetDevice(device));
-    auto* g = new (std::nothrow) ans_gpu{device, nullptr, nullptr, 0};
+    auto* g = new (std::nothrow) ans_gpu{device, nullptr, nullptr, 0, nullptr, 0};
     if (!g) return ANS_E_ALLOC;
     if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
         delete g;
@@ -1237,6 +1188,7 @@ void ans_gpu_free(ans_gpu* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     pipe_free(g);
+    if (g->d_scratch) (void)hipFree(g->d_scratch);
     (void)hipStreamDestroy(g->stream);
     delete g;
 }
@@ -1364,6 +1316,18 @@ int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const
     HIP_TRY(hipSetDevice(g->device));
     const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g->stream;
     k_compact<<<grid_for(nchunks * 64), kBlock, 0, s>>>(d_slots, slot_cap, d_lens, d_offsets, nchunks, d_out);
+    HIP_TRY(hipGetLastError());
+    return ANS_OK;
+}
+
+int ans_dev_expand(ans_gpu* g, const uint8_t* d_in, const uint64_t* d_offsets, const uint32_t* d_lens,
+                   uint64_t nchunks, uint8_t* d_slots, uint64_t slot_cap, void* stream) {
+    if (!g) return ANS_E_ARG;
+    if (nchunks == 0) return ANS_OK;
+    if (!d_in || !d_offsets || !d_lens || !d_slots) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(g->device));
+    const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g->stream;
+    k_expand<<<grid_for(nchunks * 64), kBlock, 0, s>>>(d_in, d_offsets, d_lens, nchunks, d_slots, slot_cap);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
