@@ -161,6 +161,14 @@ int ans_dev_decode_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t
  * icdf(floor(splitmix64((k << 48) ^ (start + i)) * norm / 2^64)). */
 int ans_dev_gen_iid(ans_gpu_table *gt, uint64_t seed, uint64_t start, uint64_t n, void *d_syms, int sym_bytes,
                     void *stream);
+/* Codec::samples (src/ans.rs:38-44) in bulk: chunk c of chunk_len symbols (the last may be
+ * shorter) is IID::new(codec, len).sample(seed + c), i.e. len pops from
+ * Message::random(seed + c).  The Random generator restates rand_pcg 0.3.1 Pcg64Mcg /
+ * rand_core 0.6 seed_from_u64 / rand 0.8.5 (bytes parity-unpinned: no reference test pins
+ * them), identically to the host's ANS_GEN_RANDOM. */
+int ans_dev_sample_iid(ans_gpu_table *gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void *d_syms, int sym_bytes,
+                       void *stream);
+int ans_gpu_sample_iid(ans_gpu_table *gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void *out, int sym_bytes);
 /* Compacts slot streams into a dense buffer: d_out[d_offsets[j] ..] = slot j. */
 int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const uint32_t *d_lens,
                     const uint64_t *d_offsets, uint64_t nchunks, uint8_t *d_out, void *stream);

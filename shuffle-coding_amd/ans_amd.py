@@ -82,6 +82,8 @@ SIGNATURES = {
     "ans_dev_compact": (ci, [vp, vp, u64, vp, vp, u64, vp, vp]),
     "ans_dev_status": (ci, [vp, vp, vp, ctypes.POINTER(ci)]),
     "ans_dev_expand": (ci, [vp, vp, vp, vp, u64, vp, u64, vp]),
+    "ans_dev_sample_iid": (ci, [vp, u64, u64, u64, vp, ci, vp]),
+    "ans_gpu_sample_iid": (ci, [vp, u64, u64, u64, vp, ci]),
     "ans_edge_alphabet_len": (ci, [u64, ci, ci, u64p]),
     "ans_dev_edges_to_dense": (ci, [vp, u64, ci, ci, vp, u64, vp, vp, vp]),
     "ans_dev_dense_to_edges": (ci, [vp, u64, ci, ci, vp, vp, u64, vp, vp, vp]),
@@ -617,6 +619,17 @@ class GpuTable:
         _check(lib().ans_dev_decode_chunks(self.h, _dptr(d_in), _dptr(d_offsets), slot_cap, _dptr(d_lens), n,
                                            chunk_len, gen_kind, _dptr(d_syms), sym_bytes, _dptr(d_status),
                                            _sptr(stream)), "ans_dev_decode_chunks")
+
+    def sample_chunks(self, seed, n, chunk_len, dtype=np.uint32):
+        """Codec::samples in bulk (src/ans.rs:42-44): chunk c = samples(len, seed + c)."""
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_sample_iid(self.h, seed, n, chunk_len, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
+               "ans_gpu_sample_iid")
+        return out[:n]
+
+    def dev_sample(self, seed, n, chunk_len, d_syms, sym_bytes, stream=None):
+        _check(lib().ans_dev_sample_iid(self.h, seed, n, chunk_len, _dptr(d_syms), sym_bytes, _sptr(stream)),
+               "ans_dev_sample_iid")
 
     def dev_gen_iid(self, seed, start, n, d_syms, sym_bytes, stream=None):
         _check(lib().ans_dev_gen_iid(self.h, seed, start, n, _dptr(d_syms), sym_bytes, _sptr(stream)),

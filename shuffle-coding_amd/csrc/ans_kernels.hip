@@ -276,6 +276,95 @@ __global__ __launch_bounds__(kBlock) void k_gen_iid(DevTable t, uint64_t seed, u
     }
 }
 
+// TailGenerator::Random (src/ans.rs:129-164): rand_pcg 0.3.1 Pcg64Mcg (MCG-128, XSL-RR-64
+// output) seeded by rand_core 0.6 seed_from_u64 (PCG32 expansion), one byte per draw
+// (rand 0.8.5 Standard<u8> = next_u32() as u8 = next_u64() as u8).  The same restatement as
+// the host's (ans_core.hpp TailGenerator), so GPU samples equal the host's; no reference test
+// pins these bytes (parity unpinned).
+struct Pcg64Mcg {
+    uint64_t lo, hi;
+    __device__ __forceinline__ void seed_from_u64(uint64_t st) {
+        uint32_t w[4];
+        for (int c = 0; c < 4; ++c) {
+            st = st * 6364136223846793005ull + 11634580027462260723ull;
+            const uint32_t xs = static_cast<uint32_t>(((st >> 18) ^ st) >> 27);
+            const uint32_t rot = static_cast<uint32_t>(st >> 59);
+            w[c] = (xs >> rot) | (xs << ((32 - rot) & 31));
+        }
+        lo = (static_cast<uint64_t>(w[1]) << 32 | w[0]) | 3;  // Mcg128Xsl64::new: state | 3
+        hi = static_cast<uint64_t>(w[3]) << 32 | w[2];
+    }
+    __device__ __forceinline__ uint32_t next_byte() {
+        constexpr uint64_t ML = 0x4385DF649FCCF645ull, MH = 0x2360ED051FC65DA4ull;
+        const uint64_t nlo = lo * ML;
+        hi = __umul64hi(lo, ML) + lo * MH + hi * ML;
+        lo = nlo;
+        const uint32_t rot = static_cast<uint32_t>(hi >> 58);
+        const uint64_t xsl = hi ^ lo;
+        return static_cast<uint32_t>((xsl >> rot) | (xsl << ((64 - rot) & 63))) & 0xFFu;
+    }
+};
+
+// Codec::samples (src/ans.rs:42-44) in bulk: chunk c (len = its symbol count) is
+// IID::new(codec, len).pop(&mut Message::random(seed + c)) — decoding from a message whose
+// tail is empty, so every renorm byte is drawn from the generator.
+template <typename Sym, bool kLds, bool kFast>
+__global__ __launch_bounds__(kBlock) void k_sample_iid(DevTable t, uint64_t seed, uint64_t n, uint64_t chunk_len,
+                                                       uint64_t nchunks, Sym* __restrict__ out) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const DevSym* rows = t.sym;
+    const uint16_t* bucket = t.bucket;
+    if constexpr (kLds) {
+        stage_table<true>(t, lds);
+        rows = reinterpret_cast<const DevSym*>(lds);
+        bucket = reinterpret_cast<const uint16_t*>(lds + sizeof(DevSym) * (t.nsym + 1));
+    }
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    Pcg64Mcg rng;
+    rng.seed_from_u64(seed + c);
+    uint64_t head = 1;  // Message::random (src/ans.rs:285-289): head 1, renorm_up(MAX_MIN_HEAD)
+    while (head < kMaxMinHead) head = (head << 8) | rng.next_byte();
+    const uint64_t L = t.L;
+    const uint32_t norm = t.norm;
+    auto pop = [&]() __attribute__((always_inline)) {
+        while (head < L) head = (head << 8) | rng.next_byte();  // renorm (src/ans.rs:109,239-243)
+        uint64_t q;
+        uint32_t cf;
+        if constexpr (kFast) {
+            q = quot_estimate(head, t.rcp_norm);
+            const int32_t ii = static_cast<int32_t>(static_cast<uint32_t>(head) - static_cast<uint32_t>(q) * norm);
+            if (ii < 0) { q -= 1; cf = static_cast<uint32_t>(ii) + norm; }
+            else cf = static_cast<uint32_t>(ii);
+        } else {
+            q = head / norm;
+            cf = static_cast<uint32_t>(head % norm);
+        }
+        const uint32_t s = icdf(rows, bucket, t.shift, cf);
+        const DevSym e = rows[s];
+        head = q * e.mass + (cf - e.cum);
+        return s;
+    };
+    const uint64_t a = c * chunk_len, b = min(a + chunk_len, n);
+    uint64_t k = a;
+    // whole 16-byte groups are packed in registers and stored at once (a lane's chunk is
+    // contiguous, so per-symbol stores would touch 64 cache lines per wave instruction)
+    constexpr int G = 16 / static_cast<int>(sizeof(Sym));
+    if ((a * sizeof(Sym)) % 16 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+        for (; k + G <= b; k += G) {
+            uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const uint32_t sym = pop();
+                constexpr int per = 4 / static_cast<int>(sizeof(Sym));
+                w[j / per] |= sym << (8 * sizeof(Sym) * (j % per));
+            }
+            *reinterpret_cast<uint4*>(out + k) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+    for (; k < b; ++k) out[k] = static_cast<Sym>(pop());
+}
+
 // One wave copies one stream: byte head until dst is dword-aligned, then aligned dword
 // stores funnelled from two source dwords (v_alignbyte), then the byte tail.  Source reads
 // are aligned dwords that each hold at least one byte of the stream (no over-read past the
@@ -446,6 +535,24 @@ int launch_gen(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, voi
         k_gen_iid<Sym, true><<<grid, kBlock, gt->lds_bytes, s>>>(gt->t, seed, start, n, static_cast<Sym*>(d_syms));
     else
         k_gen_iid<Sym, false><<<grid, kBlock, 0, s>>>(gt->t, seed, start, n, static_cast<Sym*>(d_syms));
+    HIP_TRY(hipGetLastError());
+    return ANS_OK;
+}
+
+template <typename Sym>
+int launch_sample(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* d_syms, hipStream_t s) {
+    const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    if (nchunks == 0) return ANS_OK;
+    const unsigned grid = grid_for(nchunks);
+    Sym* out = static_cast<Sym*>(d_syms);
+    if (gt->lds_bytes && gt->t.fast)
+        k_sample_iid<Sym, true, true><<<grid, kBlock, gt->lds_bytes, s>>>(gt->t, seed, n, chunk_len, nchunks, out);
+    else if (gt->lds_bytes)
+        k_sample_iid<Sym, true, false><<<grid, kBlock, gt->lds_bytes, s>>>(gt->t, seed, n, chunk_len, nchunks, out);
+    else if (gt->t.fast)
+        k_sample_iid<Sym, false, true><<<grid, kBlock, 0, s>>>(gt->t, seed, n, chunk_len, nchunks, out);
+    else
+        k_sample_iid<Sym, false, false><<<grid, kBlock, 0, s>>>(gt->t, seed, n, chunk_len, nchunks, out);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -1307,6 +1414,32 @@ int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n
     case 2: return launch_gen<uint16_t>(gt, seed, start, n, d_syms, s);
     default: return launch_gen<uint32_t>(gt, seed, start, n, d_syms, s);
     }
+}
+
+int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* d_syms, int sym_bytes,
+                       void* stream) {
+    if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !d_syms)) return ANS_E_ARG;
+    if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
+    if (sym_bytes == 2 && gt->t.nsym > 65536) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = pick(gt, stream);
+    switch (sym_bytes) {
+    case 1: return launch_sample<uint8_t>(gt, seed, n, chunk_len, d_syms, s);
+    case 2: return launch_sample<uint16_t>(gt, seed, n, chunk_len, d_syms, s);
+    default: return launch_sample<uint32_t>(gt, seed, n, chunk_len, d_syms, s);
+    }
+}
+
+int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* out, int sym_bytes) {
+    if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !out)) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    DevBuf d;
+    HIP_TRY(d.alloc(n * sym_bytes));
+    const int rc = ans_dev_sample_iid(gt, seed, n, chunk_len, d.p, sym_bytes, nullptr);
+    if (rc) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(out, d.p, n * sym_bytes, hipMemcpyDeviceToHost, gt->g->stream));
+    HIP_TRY(hipStreamSynchronize(gt->g->stream));
+    return ANS_OK;
 }
 
 int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const uint32_t* d_lens,

@@ -380,3 +380,35 @@ def test_host_pipeline_page_locked(sym_bytes, batch_bytes, skew, engine, monkeyp
     rc = A.lib().ans_gpu_decode_chunks(gt.h, A._np_ptr(out), len(odata), A._np_ptr(offsets), A._np_ptr(lens),
                                        n, L, A.GEN_ZEROS, A._np_ptr(back), sym_bytes)
     assert rc == A.ANS_E_MISMATCH
+
+
+# ---------------------------------------------------------------- Codec::samples in bulk
+@pytest.mark.parametrize("which", ["c3", "multiset", "tiny_norm", "big_norm", "c4"])
+def test_gpu_samples_match_host_and_oracle(gpu, which, multiset_masses):
+    """Chunk c of ans_gpu_sample_iid = IID::new(codec, len).sample(seed + c) (src/ans.rs:42-44):
+    the same symbols as the host coder and the C oracle (both Message::random, restated PCG)."""
+    rng = np.random.default_rng(17)
+    masses = {
+        "c3": A.c3_masses(),
+        "multiset": multiset_masses,
+        "tiny_norm": np.asarray([3, 0, 5, 1, 7], np.uint64),
+        "big_norm": rng.integers(1 << 22, 1 << 24, 300).astype(np.uint64),
+        "c4": A.c4_masses(),
+    }[which]
+    cat = A.Categorical(masses)
+    gt = A.GpuTable(gpu, cat)
+    n, L, seed = 5000 * 7 + 3, 5000, 1234
+    dtype = np.uint16 if len(masses) > 256 else np.uint8
+    got = gt.sample_chunks(seed, n, L, dtype)
+    ocat = orc.Categorical(masses)
+    for c in range(-(-n // L)):
+        ln = min(L, n - c * L)
+        want = ocat.pop_iid(orc.Message.random(seed + c), ln)
+        assert np.array_equal(got[c * L: c * L + ln], want.astype(dtype)), c
+        if c < 2:
+            assert A.IID(cat, ln).sample(seed + c) == [int(v) for v in want]
+    if which == "c3":  # frequencies follow the masses (loose chi-square)
+        big = gt.sample_chunks(99, 1 << 22, 4096, np.uint8)
+        cnt = np.bincount(big, minlength=256).astype(np.float64)
+        exp = masses.astype(np.float64) / masses.sum() * len(big)
+        assert ((cnt - exp) ** 2 / exp).sum() < 400  # 255 dof
