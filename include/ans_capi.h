@@ -176,6 +176,11 @@ int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const
  * fast decode kernels read). */
 int ans_dev_expand(ans_gpu *g, const uint8_t *d_in, const uint64_t *d_offsets, const uint32_t *d_lens,
                    uint64_t nchunks, uint8_t *d_slots, uint64_t slot_cap, void *stream);
+/* Test hook: the fast decoders' renorm step (renorm_up, src/ans.rs:239-243, with the next four
+ * stream bytes in the window, first byte on top) on n caller-chosen (head, window) pairs:
+ * resulting heads and byte counts.  Heads must be >= 2^24 (at most four bytes pulled). */
+int ans_dev_check_renorm(ans_gpu *g, const uint64_t *d_heads, const uint32_t *d_windows, uint64_t L, uint64_t n,
+                         uint64_t *d_out_heads, uint32_t *d_out_k, void *stream);
 /* Synchronises `stream` and maps the device status word to the lowest set status. */
 int ans_dev_status(ans_gpu *g, const uint32_t *d_status, void *stream, int *status);
 

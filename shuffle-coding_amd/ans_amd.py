@@ -83,6 +83,7 @@ SIGNATURES = {
     "ans_dev_status": (ci, [vp, vp, vp, ctypes.POINTER(ci)]),
     "ans_dev_expand": (ci, [vp, vp, vp, vp, u64, vp, u64, vp]),
     "ans_dev_sample_iid": (ci, [vp, u64, u64, u64, vp, ci, vp]),
+    "ans_dev_check_renorm": (ci, [vp, vp, vp, u64, u64, vp, vp, vp]),
     "ans_gpu_sample_iid": (ci, [vp, u64, u64, u64, vp, ci]),
     "ans_edge_alphabet_len": (ci, [u64, ci, ci, u64p]),
     "ans_dev_edges_to_dense": (ci, [vp, u64, ci, ci, vp, u64, vp, vp, vp]),

@@ -338,17 +338,33 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 // when js = 0), and k = js - 1 suffices iff X >> 8 is >= L already.  The head is >= K >= 2^25
 // after any pop in the fast range, so a zero high word means js = 4 (v_ffbh_u32(0) = ~0
 // saturates through the min).  X comes from byte permutes, exact for every js in 0..4.
-__device__ __forceinline__ uint32_t renorm_up(uint64_t& head, uint32_t W, uint64_t L) {
+//
+// X >> 8 >= L needs hi32(X >> 8) >= hi32(L), i.e. hi32(X) >= hL8 = hi32(L) << 8: the top
+// 24 bits of X all but saturated (L > 2^56 - norm).  That is ~2^-24 per symbol, so the exact
+// 64-bit test runs only when some lane of the wave passes the 32-bit screen (a uniform
+// branch; the common path is js bytes with no select).  hL8 = ~0 when L = 2^56 (hi32(L) << 8
+// would overflow, and X >> 8 < 2^56 = L never needs one byte less).
+__device__ __forceinline__ uint32_t renorm_up(uint64_t& head, uint32_t W, uint64_t L, uint32_t hL8) {
     const uint32_t h1 = hi32(head), h0 = lo32(head);
     uint32_t fb;
     asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
     const uint32_t js = min(fb >> 3, 4u);
     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(js, js, 0u);
     const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
-    const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
-    const bool one_less = js != 0 && mk64(xm1, xm0) >= L;
-    head = one_less ? mk64(xm1, xm0) : mk64(xj1, xj0);
-    return js - (one_less ? 1u : 0u);
+    head = mk64(xj1, xj0);
+    uint32_t k = js;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(xj1 >= hL8) != 0, 0)) {
+        const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
+        if (js != 0 && mk64(xm1, xm0) >= L) {
+            head = mk64(xm1, xm0);
+            k = js - 1;
+        }
+    }
+    return k;
+}
+__host__ __device__ inline uint32_t renorm_screen(uint64_t L) {
+    const uint64_t h = (L >> 32) << 8;
+    return h > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(h);
 }
 // q = head / norm, cf = head % norm (src/ans.rs:110-111): estimate, then one fix-up
 __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rcp_norm, uint64_t& qq, uint32_t& cf) {
@@ -447,9 +463,9 @@ struct DecChain {
         }
     }
     // phase 1: renorm_up, q/cf, next window
-    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
         form_window();
-        P -= static_cast<int32_t>(renorm_up(head, W, L));
+        P -= static_cast<int32_t>(renorm_up(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
@@ -510,6 +526,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     static_assert(U % SPP == 0, "points must split units evenly");
     const int nunit = static_cast<int>(chunk_len / U);
     const uint64_t L = t.L;
+    const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
@@ -541,7 +558,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
                 ch.point();
             }
             __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
-            ch.renorm_div(L, norm, rcp_norm);
+            ch.renorm_div(L, hL8, norm, rcp_norm);
 #ifdef ANS_PAD_VALU  // experiment: independent filler VALU per symbol (issue- vs latency-bound)
 #pragma unroll
             for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));
@@ -676,9 +693,9 @@ struct DecChainG {
             fetch_page(low - 2, S1);
         }
     }
-    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t norm, double rcp_norm) {
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
         form_window();
-        P -= static_cast<int32_t>(renorm_up(head, W, L));
+        P -= static_cast<int32_t>(renorm_up(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
@@ -718,6 +735,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
     static_assert(U * 4 * 4 <= 128, "a block pops at most two pages");
     const int nblocks = static_cast<int>(chunk_len / (4 * U));
     const uint64_t L = t.L;
+    const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
@@ -744,7 +762,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
             uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < U; ++j) {
-                ch.renorm_div(L, norm, rcp_norm);
+                ch.renorm_div(L, hL8, norm, rcp_norm);
                 ch.lookup(t.dbkt_g, shift);
                 if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(t.cum);
                 ch.update();

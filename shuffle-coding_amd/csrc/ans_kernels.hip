@@ -276,6 +276,19 @@ __global__ __launch_bounds__(kBlock) void k_gen_iid(DevTable t, uint64_t seed, u
     }
 }
 
+// Self-check of the decoders' renorm step (fast::renorm_up) on caller-chosen (head, window)
+// pairs, for tests: its rare exact path (X >> 8 landing in [L, 2^56)) is too rare in coded
+// data to be reached reliably (~norm / 2^56 per symbol).
+__global__ __launch_bounds__(256) void k_check_renorm(const uint64_t* __restrict__ heads,
+                                                      const uint32_t* __restrict__ windows, uint64_t L, uint64_t n,
+                                                      uint64_t* __restrict__ out_heads, uint32_t* __restrict__ out_k) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t h = heads[i];
+    out_k[i] = fast::renorm_up(h, windows[i], L, fast::renorm_screen(L));
+    out_heads[i] = h;
+}
+
 // TailGenerator::Random (src/ans.rs:129-164): rand_pcg 0.3.1 Pcg64Mcg (MCG-128, XSL-RR-64
 // output) seeded by rand_core 0.6 seed_from_u64 (PCG32 expansion), one byte per draw
 // (rand 0.8.5 Standard<u8> = next_u32() as u8 = next_u64() as u8).  The same restatement as
@@ -1414,6 +1427,17 @@ int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n
     case 2: return launch_gen<uint16_t>(gt, seed, start, n, d_syms, s);
     default: return launch_gen<uint32_t>(gt, seed, start, n, d_syms, s);
     }
+}
+
+int ans_dev_check_renorm(ans_gpu* g, const uint64_t* d_heads, const uint32_t* d_windows, uint64_t L, uint64_t n,
+                         uint64_t* d_out_heads, uint32_t* d_out_k, void* stream) {
+    if (!g || (n && (!d_heads || !d_windows || !d_out_heads || !d_out_k))) return ANS_E_ARG;
+    if (n == 0) return ANS_OK;
+    HIP_TRY(hipSetDevice(g->device));
+    const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g->stream;
+    k_check_renorm<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(d_heads, d_windows, L, n, d_out_heads, d_out_k);
+    HIP_TRY(hipGetLastError());
+    return ANS_OK;
 }
 
 int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* d_syms, int sym_bytes,

@@ -412,3 +412,56 @@ def test_gpu_samples_match_host_and_oracle(gpu, which, multiset_masses):
         cnt = np.bincount(big, minlength=256).astype(np.float64)
         exp = masses.astype(np.float64) / masses.sum() * len(big)
         assert ((cnt - exp) ** 2 / exp).sum() < 400  # 255 dof
+
+
+# ---------------------------------------------------------------- renorm step, adversarial
+def _renorm_ref(head, window, L):
+    """renorm_up (src/ans.rs:239-243): pull bytes (the window's top byte first) while head < L."""
+    k = 0
+    while head < L:
+        head = ((head << 8) | ((window >> (24 - 8 * k)) & 0xFF)) & ((1 << 64) - 1)
+        k += 1
+    return head, k
+
+
+@pytest.mark.parametrize("norm", [139_224_331, 268_434_941, (1 << 16) + 1, (1 << 31) - 1, 1 << 24, 3 * 5 ** 11])
+def test_fast_renorm_exact_in_the_rare_window(gpu, norm):
+    """The decoders take js = clz(head)/8 bytes unless X >> 8 already reaches L, which needs X in
+    a window of width 2^56 mod norm (renorm_up's voted exact path): heads built to land there,
+    mixed in the same waves with ordinary heads."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(norm % 1000)
+    K = (1 << 56) // norm
+    L = norm * K
+    heads, wins = [], []
+    for i in range(4096):
+        w = int(rng.integers(0, 1 << 32))
+        kind = i % 4
+        if kind == 0:  # ordinary head after a pop, below L
+            h = int(rng.integers(1 << 24, L))
+        else:  # js = kind bytes, and X >> 8 inside [L, 2^56) or just below L
+            js = kind
+            lo = -(-(L - ((1 << (8 * (js - 1))) - 1)) // (1 << (8 * (js - 1))))  # head << 8(js-1) | ones >= L
+            hi = 1 << (64 - 8 * js)
+            h = int(rng.integers(max(lo - 3, 1 << 24), hi)) if hi > lo else int(rng.integers(1 << 24, hi))
+            if rng.random() < 0.5:
+                w = (1 << 32) - 1 - int(rng.integers(0, 256))  # top bytes near 0xFF: X >> 8 at the edge
+        heads.append(min(h, (1 << 64) - 1))
+        wins.append(w)
+    d_h = torch.tensor(np.asarray(heads, np.uint64).view(np.int64), device="cuda")
+    d_w = torch.tensor(np.asarray(wins, np.uint32).view(np.int32), device="cuda")
+    o_h = torch.empty_like(d_h)
+    o_k = torch.empty_like(d_w)
+    A._check(A.lib().ans_dev_check_renorm(gpu.h, d_h.data_ptr(), d_w.data_ptr(), L, len(heads), o_h.data_ptr(),
+                                          o_k.data_ptr(), None), "check_renorm")
+    torch.cuda.synchronize()
+    gh = o_h.cpu().numpy().view(np.uint64)
+    gk = o_k.cpu().numpy().view(np.uint32)
+    rare = 0
+    for i, (h, w) in enumerate(zip(heads, wins)):
+        eh, ek = _renorm_ref(h, w, L)
+        assert (int(gh[i]), int(gk[i])) == (eh, ek), (i, hex(h), hex(w))
+        js = min((64 - h.bit_length()) // 8, 4)
+        rare += ek == js - 1 and js > 0
+    if (1 << 56) - L > 0:
+        assert rare > 100  # the exact path was exercised
