@@ -497,13 +497,27 @@ struct DecChain {
             nxt = lcum[sx + 1];
         }
     }
-    // phase 3: head = p*q + r (src/ans.rs:113-114)
-    __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
+    // phase 3: head = p*q + r (src/ans.rs:113-114).  With every mass below 2^24 (kP24) the
+    // high word's product hi32(q) * p (hi32(q) < 2^16 in the fast range) is one full-rate
+    // v_mad_u32_u24 instead of a second v_mad_u64_u32.
+    template <bool kP24>
+    __device__ __forceinline__ void update() {
+        const uint32_t p = nxt - cum, a = cf - cum;
+        if constexpr (kP24) {
+            const uint64_t lo = static_cast<uint64_t>(lo32(qq)) * p + a;
+            uint32_t hi;
+            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(hi) : "v"(hi32(qq)), "v"(p), "v"(hi32(lo)));
+            head = mk64(hi, lo32(lo));
+        } else {
+            head = qq * p + a;
+        }
+    }
 };
 
 // SPP: symbols per point (U, or U/2 when U*KMAX > 60: u8 tables whose pops can take 4 bytes).
 // kFar: some bucket holds more than four cdf boundaries, so the voted slow path is compiled in.
-template <typename Sym, int SPP, bool kFar>
+// kP24: every mass is below 2^24 (DecChain::update).
+template <typename Sym, int SPP, bool kFar, bool kP24>
 __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
@@ -565,7 +579,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
 #endif
             ch.lookup(lds, shift);
             if (kFar && __builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
-            ch.update();
+            ch.template update<kP24>();
             put_sym<Sym>(outv, j, ch.sx);
         }
         switch (u & 3) {

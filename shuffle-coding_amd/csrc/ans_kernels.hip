@@ -514,12 +514,14 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
                 fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
-#define DEC(SPP, FAR) fast::k_decode<Sym, SPP, FAR><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
+#define DEC(SPP, FAR, P24) fast::k_decode<Sym, SPP, FAR, P24><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
+#define DEC_P(SPP, FAR) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true); else DEC(SPP, FAR, false)
             if (U * ft.kmax > 60) {
-                if (ft.dec_far) DEC(U / 2, true); else DEC(U / 2, false);
+                if (ft.dec_far) { DEC_P(U / 2, true); } else { DEC_P(U / 2, false); }
             } else {
-                if (ft.dec_far) DEC(U, true); else DEC(U, false);
+                if (ft.dec_far) { DEC_P(U, true); } else { DEC_P(U, false); }
             }
+#undef DEC_P
 #undef DEC
         }
         HIP_TRY(hipGetLastError());
@@ -652,6 +654,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_cum_off = static_cast<uint32_t>((sizeof(DecBucket) * dec.size() + 15) & ~size_t(15));
     ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;
+    ft.pmax = 0;
+    for (uint32_t s = 0; s < nsym; ++s) ft.pmax = std::max<uint32_t>(ft.pmax, static_cast<uint32_t>(cat.masses[s]));
     ft.K = t.K;
     ft.L = t.L;
     ft.rcp_norm = t.rcp_norm;

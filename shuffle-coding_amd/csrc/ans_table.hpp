@@ -79,6 +79,7 @@ struct FastTable {
     uint32_t dec_lds_bytes;   // LDS bytes of the staged decode buckets + cdf table (16-aligned)
     uint32_t dec_cum_off;     // LDS offset of the cdf table
     uint32_t kmax;            // max bytes one push (and so one pop) moves (1..4)
+    uint32_t pmax;            // largest mass (decode picks a 24-bit multiply below 2^24)
     uint64_t K;
     uint64_t L;
     double rcp_norm;

@@ -465,3 +465,33 @@ def test_fast_renorm_exact_in_the_rare_window(gpu, norm):
         rare += ek == js - 1 and js > 0
     if (1 << 56) - L > 0:
         assert rare > 100  # the exact path was exercised
+
+
+# ---------------------------------------------------------------- table-shape boundaries
+def _tables_at_the_boundaries():
+    rng = np.random.default_rng(23)
+
+    def spread(nsym, norm):  # nsym positive masses summing exactly to norm
+        cuts = np.sort(rng.choice(np.arange(1, norm), nsym - 1, replace=False)) if nsym > 1 else np.array([], int)
+        return np.diff(np.concatenate([[0], cuts, [norm]])).astype(np.uint64)
+
+    return {
+        "norm_2^16": spread(256, 1 << 16),             # bottom of the fast range
+        "norm_2^16-1": spread(256, (1 << 16) - 1),     # just below: generic kernels
+        "norm_2^31": spread(256, 1 << 31),             # top of the fast range, L = 2^56
+        "norm_2^31+1": spread(256, (1 << 31) + 1),     # just above: generic kernels
+        "norm_2^32-1": spread(97, (1 << 32) - 1),      # largest norm the GPU takes
+        "one_symbol": np.asarray([1 << 20], np.uint64),  # p = norm: nothing is ever emitted
+        "kmax_4": np.concatenate([[1, 1, 2], spread(200, (1 << 31) - 4)]).astype(np.uint64),  # 4-byte pushes
+        "pow2_norm_2^24": spread(256, 1 << 24),        # L = 2^56 exactly (empty renorm window)
+    }
+
+
+@pytest.mark.parametrize("name", list(_tables_at_the_boundaries()))
+def test_boundary_tables_bit_exact(gpu, name):
+    masses = _tables_at_the_boundaries()[name]
+    rng = np.random.default_rng(len(name))
+    nz = np.flatnonzero(masses)
+    # uniform over the symbols, so the rare (tiny-mass) symbols are coded often
+    syms = rng.choice(nz, size=520 * 4096 + 77).astype(np.uint32)
+    _roundtrip_vs_oracle(gpu, masses, syms, 4096, np.uint8 if len(masses) <= 256 else np.uint16)
