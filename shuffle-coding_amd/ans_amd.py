@@ -344,6 +344,42 @@ class Uniform(Distribution):  # src/codec.rs:13-49
         return math.log2(self.size)
 
 
+class LogUniform(Codec):  # src/codec.rs:561-611 (MaxBenfordIID's item, src/param_codec.rs:117-119)
+    """x's bit length is Uniform over [0, excl_max_bits]; the bits below the top one are
+    Uniform(2^(bits-1)), pushed first."""
+
+    def __init__(self, excl_max_bits):
+        assert excl_max_bits <= 64
+        self.bits_codec = Uniform(excl_max_bits + 1)
+
+    @classmethod
+    def max(cls):  # LogUniform::new(47)
+        return cls(47)
+
+    @staticmethod
+    def get_bits(x):
+        return int(x).bit_length()
+
+    def push(self, m, x):
+        b = self.get_bits(x)
+        assert b < self.bits_codec.size
+        if b:
+            size = 1 << (b - 1)
+            Uniform(size).push(m, int(x) & ~size)
+        self.bits_codec.push(m, b)
+
+    def pop(self, m):
+        b = self.bits_codec.pop(m)
+        if b == 0:
+            return 0
+        size = 1 << (b - 1)
+        return Uniform(size).pop(m) | size
+
+    def bits(self, x):
+        b = self.get_bits(x)
+        return self.bits_codec.uni_bits() + (Uniform(1 << (b - 1)).uni_bits() if b else 0.0)
+
+
 class Categorical(Distribution):  # src/codec.rs:51-92
     def __init__(self, masses):
         self.masses = np.ascontiguousarray(np.asarray(masses, dtype=np.uint64))

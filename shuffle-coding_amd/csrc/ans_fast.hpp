@@ -76,6 +76,11 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t off) { return *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(off)); }
 __device__ __forceinline__ uint64_t lds_ld64(uint32_t off) { return *reinterpret_cast<const lds_u64*>(static_cast<uintptr_t>(off)); }
+typedef __attribute__((address_space(3))) v4u32 lds_v4u32;
+__device__ __forceinline__ uint4 lds_ld128(uint32_t off) {
+    const v4u32 v = *reinterpret_cast<const lds_v4u32*>(static_cast<uintptr_t>(off));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // (kept at LDS offset 0: a row address is one v_and_or of the row bits and the lane's column)
 struct Ring {
@@ -470,26 +475,26 @@ struct DecChain {
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
     }
-    // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket
-    __device__ __forceinline__ void lookup(const unsigned char* lds, uint32_t shift) {
-        // bucket address = (cf >> shift) * 24 + table base: one v_mad_u32_u24 (kept whole: the
-        // compiler otherwise splits the base out into two adds, as it exceeds the ds offset)
-        uint32_t off;
-        asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(off) : "v"(cf >> shift), "s"(kDecRingBytes));
-        uint64_t r01 = lds_ld64(off), r23 = lds_ld64(off + 8), r4s = lds_ld64(off + 16);
-        // all three reads complete here: the compiler otherwise defers the ones a select needs
-        // only on some lanes into branches, adding dependent LDS round trips
-        asm volatile("" ::"v"(r01), "v"(r23), "v"(r4s));
-        const uint2 e01 = make_uint2(lo32(r01), hi32(r01)), e23 = make_uint2(lo32(r23), hi32(r23)),
-                    e4s = make_uint2(lo32(r4s), hi32(r4s));
-        const bool b1 = cf >= e01.y, b2 = cf >= e23.x, b3 = cf >= e23.y;
-        cum = b3 ? e23.y : (b2 ? e23.x : (b1 ? e01.y : e01.x));
-        nxt = b3 ? e4s.x : (b2 ? e23.y : (b1 ? e23.x : e01.y));
-        sx = e4s.y + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
-        asm volatile("" : "+v"(sx));  // now, not at the unit's end (its compare masks would spill)
-        far = cf >= e4s.x;
+    // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket:
+    // c0..c3 in one ds_read_b128 (two compares pick among three candidates; cf >= c3 is the
+    // voted far case), s0 from the array after the buckets.
+    __device__ __forceinline__ void lookup(uint32_t shift, uint32_t s0_base) {
+        const uint32_t bi = cf >> shift;
+        uint32_t off, soff;  // table bases exceed the ds offset field: one v_lshl_add each
+        asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(off) : "v"(bi), "s"(kDecRingBytes));
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(soff) : "v"(bi), "s"(s0_base));
+        const uint4 c = lds_ld128(off);
+        const uint32_t s0 = lds_ld32(soff);
+        // the read completes here: the compiler otherwise defers parts a select needs only on
+        // some lanes into branches, adding dependent LDS round trips
+        asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
+        const bool b1 = cf >= c.y, b2 = cf >= c.z;
+        cum = b2 ? c.z : (b1 ? c.y : c.x);
+        nxt = b2 ? c.w : (b1 ? c.z : c.y);
+        sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u);
+        far = cf >= c.w;
     }
-    __device__ __forceinline__ void lookup_far(const uint32_t* lcum) {  // 4+ boundaries in the bucket
+    __device__ __forceinline__ void lookup_far(const uint32_t* lcum) {  // 3+ boundaries in the bucket
         if (far) {
             sx += 1;
             while (cf >= lcum[sx + 1]) ++sx;
@@ -525,9 +530,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     extern __shared__ __align__(16) unsigned char lds[];
     unsigned char* tab = lds + kDecRingBytes;  // ring at offset 0, tables after it
     {
-        uint2* b = reinterpret_cast<uint2*>(tab);
-        const uint2* gb = reinterpret_cast<const uint2*>(t.dbkt);
-        for (uint32_t i = threadIdx.x; i < 3 * t.dec_buckets; i += kBlock) b[i] = gb[i];
+        uint4* b = reinterpret_cast<uint4*>(tab);  // buckets and s0 array: dec_cum_off bytes
+        const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt);
+        for (uint32_t i = threadIdx.x; i < t.dec_cum_off / 16; i += kBlock) b[i] = gb[i];
         uint32_t* cl = reinterpret_cast<uint32_t*>(tab + t.dec_cum_off);
         for (uint32_t i = threadIdx.x; i < t.nsym + 5; i += kBlock) cl[i] = t.cum[i];
     }
@@ -544,6 +549,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
+    const uint32_t s0_base = kDecRingBytes + t.dec_s0_off;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
 #ifdef ANS_PAD_VALU
@@ -577,7 +583,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
 #pragma unroll
             for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));
 #endif
-            ch.lookup(lds, shift);
+            ch.lookup(shift, s0_base);
             if (kFar && __builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
             ch.template update<kP24>();
             put_sym<Sym>(outv, j, ch.sx);

@@ -216,6 +216,7 @@ int ans_edge_alphabet_len(uint64_t num_nodes, int directed, int loops, uint64_t*
 
 int ans_dev_edges_to_dense(ans_gpu* g, uint64_t num_nodes, int directed, int loops, const uint32_t* d_edges,
                            uint64_t num_edges, uint8_t* d_dense, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g || !d_status || !valid_space(num_nodes) || (num_edges && !d_edges)) return ANS_E_ARG;
     const EdgeSpace e{num_nodes, directed ? 1u : 0u, loops ? 1u : 0u};
     const uint64_t len = alphabet_len(e);
@@ -232,6 +233,7 @@ int ans_dev_edges_to_dense(ans_gpu* g, uint64_t num_nodes, int directed, int loo
 
 int ans_dev_dense_to_edges(ans_gpu* g, uint64_t num_nodes, int directed, int loops, const uint8_t* d_dense,
                            uint32_t* d_edges, uint64_t cap, uint64_t* d_count, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g || !d_status || !d_count || !valid_space(num_nodes) || (cap && !d_edges)) return ANS_E_ARG;
     const EdgeSpace e{num_nodes, directed ? 1u : 0u, loops ? 1u : 0u};
     const uint64_t len = alphabet_len(e);
@@ -265,6 +267,7 @@ int ans_dev_dense_to_edges(ans_gpu* g, uint64_t num_nodes, int directed, int loo
 int ans_gpu_dense_set_encode(ans_gpu_table* gt, uint64_t num_nodes, int directed, int loops, const uint32_t* edges,
                              uint64_t num_edges, uint64_t chunk_len, uint8_t* out, uint64_t out_cap,
                              uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !total || chunk_len == 0 || !valid_space(num_nodes) || (num_edges && !edges)) return ANS_E_ARG;
     if (gt->t.nsym != 2) return ANS_E_ARG;  // a Bernoulli table
     const EdgeSpace e{num_nodes, directed ? 1u : 0u, loops ? 1u : 0u};
@@ -323,6 +326,7 @@ int ans_gpu_dense_set_encode(ans_gpu_table* gt, uint64_t num_nodes, int directed
 int ans_gpu_dense_set_decode(ans_gpu_table* gt, uint64_t num_nodes, int directed, int loops, const uint8_t* in,
                              uint64_t in_len, const uint64_t* offsets, const uint64_t* lens, uint64_t chunk_len,
                              uint32_t* edges, uint64_t cap, uint64_t* num_edges) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !num_edges || chunk_len == 0 || !valid_space(num_nodes) || (cap && !edges)) return ANS_E_ARG;
     if (gt->t.nsym != 2) return ANS_E_ARG;
     const EdgeSpace e{num_nodes, directed ? 1u : 0u, loops ? 1u : 0u};

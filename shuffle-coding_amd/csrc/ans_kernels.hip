@@ -621,22 +621,24 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         const char* e = getenv("ANS_DECG_BUCKET_BITS");
         return e ? static_cast<uint32_t>(atoi(e)) : 16u;
     }();
-    const uint64_t max_buckets = ft.dec_usable ? (fast::kDecTableBytes - cum_bytes) / sizeof(DecBucket) : (1ull << g_bits);
+    const uint64_t max_buckets =
+        ft.dec_usable ? (fast::kDecTableBytes - cum_bytes - 16) / (sizeof(DecBucket) + sizeof(uint32_t)) : (1ull << g_bits);
     while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > max_buckets) ++shift;
     const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1);
     std::vector<uint32_t> cum(nsym + 6, t.norm);
     for (uint32_t s = 0; s < nsym; ++s) cum[s] = static_cast<uint32_t>(cat.cummasses[s]);
     std::vector<DecBucket> dec(ft.dec_usable ? nb : 0);
+    std::vector<uint32_t> dec_s0(ft.dec_usable ? nb : 0);
     std::vector<DecBucketG> decg(ft.dec_usable ? 0 : nb);
     for (uint32_t j = 0; j < nb; ++j) {
         const uint32_t s0 = static_cast<uint32_t>(cat.icdf(static_cast<uint64_t>(j) << shift).first);
         if (ft.dec_usable) {
             DecBucket& d = dec[j];
-            for (int i = 0; i < 5; ++i) d.c[i] = cum[s0 + i];
-            d.s0 = s0;
-            // every cf of the bucket below cdf(s0 + 4)?  (the last bucket ends at norm)
+            for (int i = 0; i < 4; ++i) d.c[i] = cum[s0 + i];
+            dec_s0[j] = s0;
+            // every cf of the bucket below cdf(s0 + 3)?  (the last bucket ends at norm)
             const uint64_t end = std::min<uint64_t>(t.norm, (static_cast<uint64_t>(j) + 1) << shift);
-            if (d.c[4] < end) ft.dec_far = 1;
+            if (d.c[3] < end) ft.dec_far = 1;
         } else {
             DecBucketG& d = decg[j];
             for (int i = 0; i < 6; ++i) d.c[i] = cum[s0 + i];
@@ -651,7 +653,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_shift = shift;
     ft.norm = t.norm;
     ft.enc_lds_bytes = fast::kEncLdsBytes;  // nsym + 1 <= 257 rows, split (ans_fast.hpp)
-    ft.dec_cum_off = static_cast<uint32_t>((sizeof(DecBucket) * dec.size() + 15) & ~size_t(15));
+    ft.dec_s0_off = static_cast<uint32_t>(sizeof(DecBucket) * dec.size());
+    ft.dec_cum_off = static_cast<uint32_t>((ft.dec_s0_off + sizeof(uint32_t) * dec_s0.size() + 15) & ~size_t(15));
     ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;
     ft.pmax = 0;
@@ -659,7 +662,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.K = t.K;
     ft.L = t.L;
     ft.rcp_norm = t.rcp_norm;
-    const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = sizeof(DecBucket) * dec.size();
+    const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = ft.dec_cum_off;  // buckets + s0 array
     const size_t decg_b = sizeof(DecBucketG) * decg.size();
     const size_t o_dec = (enc_b + 255) & ~size_t(255), o_cum = o_dec + ((dec_b + 255) & ~size_t(255));
     const size_t o_decg = o_cum + ((sizeof(uint32_t) * cum.size() + 255) & ~size_t(255));
@@ -669,7 +672,10 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(base + o_dec, dec.data(), dec_b, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_dec, dec.data(), sizeof(DecBucket) * dec.size(), hipMemcpyHostToDevice));
+    if (!dec_s0.empty())
+        HIP_TRY(hipMemcpy(base + o_dec + ft.dec_s0_off, dec_s0.data(), sizeof(uint32_t) * dec_s0.size(),
+                          hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_cum, cum.data(), sizeof(uint32_t) * cum.size(), hipMemcpyHostToDevice));
     if (decg_b) HIP_TRY(hipMemcpy(base + o_decg, decg.data(), decg_b, hipMemcpyHostToDevice));
     ft.dbkt_g = reinterpret_cast<const DecBucketG*>(base + o_decg);
@@ -1392,6 +1398,7 @@ int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t*
 
 int ans_dev_encode_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                           uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0 || (slot_cap & 15)) return ANS_E_ARG;
     if (n && (!d_syms || !d_slots || !d_lens)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
@@ -1406,6 +1413,7 @@ int ans_dev_encode_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, 
 int ans_dev_decode_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                           const uint32_t* d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* d_syms,
                           int sym_bytes, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0) return ANS_E_ARG;
     if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;
     if (n && (!d_in || !d_lens || !d_syms)) return ANS_E_ARG;
@@ -1422,6 +1430,7 @@ int ans_dev_decode_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t
 
 int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, void* d_syms, int sym_bytes,
                     void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || (n && !d_syms)) return ANS_E_ARG;
     if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
@@ -1435,6 +1444,7 @@ int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n
 
 int ans_dev_check_renorm(ans_gpu* g, const uint64_t* d_heads, const uint32_t* d_windows, uint64_t L, uint64_t n,
                          uint64_t* d_out_heads, uint32_t* d_out_k, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g || (n && (!d_heads || !d_windows || !d_out_heads || !d_out_k))) return ANS_E_ARG;
     if (n == 0) return ANS_OK;
     HIP_TRY(hipSetDevice(g->device));
@@ -1446,6 +1456,7 @@ int ans_dev_check_renorm(ans_gpu* g, const uint64_t* d_heads, const uint32_t* d_
 
 int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* d_syms, int sym_bytes,
                        void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !d_syms)) return ANS_E_ARG;
     if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
     if (sym_bytes == 2 && gt->t.nsym > 65536) return ANS_E_ARG;
@@ -1459,6 +1470,7 @@ int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
 }
 
 int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* out, int sym_bytes) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !out)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     DevBuf d;
@@ -1472,6 +1484,7 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
 
 int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const uint32_t* d_lens,
                     const uint64_t* d_offsets, uint64_t nchunks, uint8_t* d_out, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g) return ANS_E_ARG;
     if (nchunks == 0) return ANS_OK;
     HIP_TRY(hipSetDevice(g->device));
@@ -1483,6 +1496,7 @@ int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const
 
 int ans_dev_expand(ans_gpu* g, const uint8_t* d_in, const uint64_t* d_offsets, const uint32_t* d_lens,
                    uint64_t nchunks, uint8_t* d_slots, uint64_t slot_cap, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g) return ANS_E_ARG;
     if (nchunks == 0) return ANS_OK;
     if (!d_in || !d_offsets || !d_lens || !d_slots) return ANS_E_ARG;
@@ -1506,6 +1520,7 @@ int ans_dev_status(ans_gpu* g, const uint32_t* d_status, void* stream, int* stat
 
 int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                           uint8_t* out, uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || !total) return ANS_E_ARG;
     if (n && !syms) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
@@ -1533,6 +1548,7 @@ int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, ui
 int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                           const uint64_t* lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* out,
                           int sym_bytes) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks && (!in || !offsets || !lens || !out)) return ANS_E_ARG;

@@ -50,13 +50,14 @@ struct EncRow {
     uint32_t mass;
     uint32_t cum;
 };
-// Decode bucket (24 B, three ds_read_b64): bucket j covers cdf values [j << dec_shift,
-// (j+1) << dec_shift).  s0 = icdf(j << dec_shift) and c[i] = cdf(s0 + i), i = 0..4 (norm past
-// the last symbol), so one LDS round trip resolves every cf in the bucket below c[4]; the
-// rest (a bucket holding four or more boundaries) scan the cdf table staged after the buckets.
-struct alignas(8) DecBucket {
-    uint32_t c[5];
-    uint32_t s0;
+// Decode bucket (16 B, one ds_read_b128): bucket j covers cdf values [j << dec_shift,
+// (j+1) << dec_shift).  s0 = icdf(j << dec_shift) and c[i] = cdf(s0 + i), i = 0..3 (norm past
+// the last symbol), so one LDS round trip resolves every cf in the bucket below c[3]; the
+// rest (a bucket holding three or more boundaries, voted per wave) scan the cdf table staged
+// after the buckets.  The s0 values follow the buckets as a u32 array (read off the chain's
+// critical path: they only name the output symbol).
+struct alignas(16) DecBucket {
+    uint32_t c[4];
 };
 // Decode bucket for large alphabets (32 B, two 16-B global loads): cdf(s0..s0+5) and s0, so
 // five candidates per bucket.
@@ -67,7 +68,7 @@ struct alignas(16) DecBucketG {
 };
 struct FastTable {
     const EncRow* enc;        // enc_rows = nsym + 1 rows (last = zero-mass sentinel)
-    const DecBucket* dbkt;    // dec_buckets entries
+    const DecBucket* dbkt;    // dec_buckets entries, then dec_buckets u32 s0 values (16-aligned region)
     const uint32_t* cum;      // cdf(s) for s = 0..nsym+5 (norm from nsym on): the slow icdf path
     const DecBucketG* dbkt_g; // large alphabets: dec_buckets entries in global memory
     uint32_t nsym;
@@ -77,6 +78,7 @@ struct FastTable {
     uint32_t dec_shift;
     uint32_t enc_lds_bytes;   // LDS bytes of the staged encode rows (16-aligned)
     uint32_t dec_lds_bytes;   // LDS bytes of the staged decode buckets + cdf table (16-aligned)
+    uint32_t dec_s0_off;      // offset of the s0 array from the buckets (LDS and global)
     uint32_t dec_cum_off;     // LDS offset of the cdf table
     uint32_t kmax;            // max bytes one push (and so one pop) moves (1..4)
     uint32_t pmax;            // largest mass (decode picks a 24-bit multiply below 2^24)
@@ -87,7 +89,7 @@ struct FastTable {
     uint32_t enc_global;  // rows read from global memory (nsym > 256; ans_fast.hpp kGlobalRows)
     uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
     uint32_t dec_global;  // decode fast path for nsym > 256 (k_decode_g, buckets in global memory)
-    uint32_t dec_far;     // some LDS bucket holds more than four cdf boundaries (slow path needed)
+    uint32_t dec_far;     // some LDS bucket holds three or more cdf boundaries (slow path needed)
 };
 
 }  // namespace shuffle_coding

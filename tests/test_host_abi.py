@@ -172,3 +172,27 @@ def test_message_equality_canonicalises():
     assert r == r.reflatten()
     assert r != A.Message.random(4)
     assert A.Message.zeros() != A.Message.empty()
+
+
+def test_truncated_benford_log_uniform():
+    # src/codec.rs:663-669: LogUniform::new(8) passes Codec::test for x < 255 from Message::random(0);
+    # bytes equal the oracle's composition of Uniform pushes (src/codec.rs:569-577)
+    c = A.LogUniform(8)
+    for i in range(255):
+        c.test(i, A.Message.random(0))
+    m = A.Message.zeros()
+    om = orc.Message.zeros()
+    xs = [0, 1, 2, 3, 7, 8, 200, 254, 100, 5]
+    for x in xs:
+        c.push(m, x)
+        b = x.bit_length()
+        if b:
+            assert orc.uniform_push(om, 1 << (b - 1), x & ~(1 << (b - 1))) == 0
+        assert orc.uniform_push(om, 9, b) == 0
+    assert m.flatten() == om.flatten()
+    assert [c.pop(m) for _ in xs] == xs[::-1]
+    big = A.LogUniform.max()  # MaxBenfordIID's item: 47-bit values
+    m = A.Message.zeros()
+    for x in [(1 << 46) + 12345, 1, 0, (1 << 40) - 1]:
+        big.push(m, x)
+        assert big.pop(m) == x
