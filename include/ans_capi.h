@@ -169,6 +169,23 @@ int ans_dev_gen_iid(ans_gpu_table *gt, uint64_t seed, uint64_t start, uint64_t n
 int ans_dev_sample_iid(ans_gpu_table *gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void *d_syms, int sym_bytes,
                        void *stream);
 int ans_gpu_sample_iid(ans_gpu_table *gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void *out, int sym_bytes);
+/* Variable-length chunks: chunk c is symbols [starts[c], starts[c+1]) (nchunks + 1
+ * non-decreasing entries), still one reference message each, e.g. one graph or one record per
+ * chunk.  Generic kernels, one lane per chunk; slot_cap = ans_gpu_slot_capacity of the longest
+ * chunk.  Symbols live at their absolute index (the buffers span [0, starts[nchunks])). */
+int ans_dev_encode_var_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t nchunks,
+                              const uint64_t *d_starts, uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens,
+                              uint32_t *d_status, void *stream);
+/* d_offsets == NULL: chunk c's stream at d_in + c*slot_cap; else at d_in + d_offsets[c] */
+int ans_dev_decode_var_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
+                              const uint32_t *d_lens, uint64_t nchunks, const uint64_t *d_starts, int gen_kind,
+                              void *d_syms, int sym_bytes, uint32_t *d_status, void *stream);
+int ans_gpu_encode_var_chunks(ans_gpu_table *gt, const void *syms, int sym_bytes, uint64_t nchunks,
+                              const uint64_t *starts, uint8_t *out, uint64_t out_cap, uint64_t *offsets,
+                              uint64_t *lens, uint64_t *total);
+int ans_gpu_decode_var_chunks(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
+                              const uint64_t *lens, uint64_t nchunks, const uint64_t *starts, int gen_kind, void *out,
+                              int sym_bytes);
 /* Compacts slot streams into a dense buffer: d_out[d_offsets[j] ..] = slot j. */
 int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const uint32_t *d_lens,
                     const uint64_t *d_offsets, uint64_t nchunks, uint8_t *d_out, void *stream);
@@ -212,6 +229,20 @@ int ans_gpu_dense_set_encode(ans_gpu_table *gt, uint64_t num_nodes, int directed
 int ans_gpu_dense_set_decode(ans_gpu_table *gt, uint64_t num_nodes, int directed, int loops, const uint8_t *in,
                              uint64_t in_len, const uint64_t *offsets, const uint64_t *lens, uint64_t chunk_len,
                              uint32_t *edges, uint64_t cap, uint64_t *num_edges);
+
+/* Independent<GraphIID<ErdosRenyi>> over a dataset of graphs (GraphDatasetParamCodec with
+ * ErdosRenyiParamCodec: one Bernoulli gt for every graph, src/param_codec.rs:171-199,243-293).
+ * Graph g has num_nodes[g] nodes and the edges [edge_offsets[g], edge_offsets[g+1]) of `edges`
+ * (uint32 pairs).  Graph g is chunk g of the variable-chunk path: its stream is the reference
+ * message Message::zeros() + ErdosRenyi push of that graph alone.  Decode returns every graph's
+ * edges in alphabet order, graph after graph, with edge_offsets (num_graphs + 1 entries) giving
+ * each graph's range; ANS_E_LEN when they exceed cap (edge_offsets still complete). */
+int ans_gpu_dense_sets_encode(ans_gpu_table *gt, uint64_t num_graphs, const uint32_t *num_nodes, int directed,
+                              int loops, const uint32_t *edges, const uint64_t *edge_offsets, uint8_t *out,
+                              uint64_t out_cap, uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_dense_sets_decode(ans_gpu_table *gt, uint64_t num_graphs, const uint32_t *num_nodes, int directed,
+                              int loops, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
+                              const uint64_t *lens, uint32_t *edges, uint64_t cap, uint64_t *edge_offsets);
 
 #ifdef __cplusplus
 }

@@ -90,6 +90,12 @@ SIGNATURES = {
     "ans_dev_dense_to_edges": (ci, [vp, u64, ci, ci, vp, vp, u64, vp, vp, vp]),
     "ans_gpu_dense_set_encode": (ci, [vp, u64, ci, ci, vp, u64, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_dense_set_decode": (ci, [vp, u64, ci, ci, vp, u64, vp, vp, u64, vp, u64, u64p]),
+    "ans_dev_encode_var_chunks": (ci, [vp, vp, ci, u64, vp, vp, u64, vp, vp, vp]),
+    "ans_dev_decode_var_chunks": (ci, [vp, vp, vp, u64, vp, u64, vp, ci, vp, ci, vp, vp]),
+    "ans_gpu_encode_var_chunks": (ci, [vp, vp, ci, u64, vp, vp, u64, vp, vp, u64p]),
+    "ans_gpu_decode_var_chunks": (ci, [vp, vp, u64, vp, vp, u64, vp, ci, vp, ci]),
+    "ans_gpu_dense_sets_encode": (ci, [vp, u64, vp, ci, ci, vp, vp, vp, u64, vp, vp, u64p]),
+    "ans_gpu_dense_sets_decode": (ci, [vp, u64, vp, ci, ci, vp, u64, vp, vp, vp, u64, vp]),
 }
 
 _lib = None
@@ -646,6 +652,35 @@ class GpuTable:
                                            _WIDTH[np.dtype(dtype)]), "ans_gpu_decode_chunks")
         return out[:n]
 
+    def encode_var_chunks(self, syms, starts):
+        """Variable-length chunks: chunk c = syms[starts[c]:starts[c+1]], one reference message
+        each.  Returns (dense bytes, offsets u64, lens u64)."""
+        syms = np.ascontiguousarray(syms)
+        starts = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
+        nchunks = len(starts) - 1
+        longest = int(np.diff(starts).max()) if nchunks else 0
+        out = np.empty(max(nchunks * self.slot_capacity(longest), 1), np.uint8)
+        offsets = np.zeros(max(nchunks, 1), np.uint64)
+        lens = np.zeros(max(nchunks, 1), np.uint64)
+        total = u64(0)
+        _check(lib().ans_gpu_encode_var_chunks(self.h, _np_ptr(syms), _WIDTH[syms.dtype], nchunks, _np_ptr(starts),
+                                               _np_ptr(out), len(out), _np_ptr(offsets), _np_ptr(lens),
+                                               ctypes.byref(total)), "ans_gpu_encode_var_chunks")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode_var_chunks(self, data, offsets, lens, starts, dtype=np.uint32, gen_kind=GEN_ZEROS):
+        data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+        offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        starts = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
+        n = int(starts[-1]) if len(starts) else 0
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_decode_var_chunks(self.h, _np_ptr(data) if data.size else None, data.size,
+                                               _np_ptr(offsets), _np_ptr(lens), len(starts) - 1, _np_ptr(starts),
+                                               gen_kind, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
+               "ans_gpu_decode_var_chunks")
+        return out[:n]
+
     # ---- device buffers (torch tensors or raw pointers)
     def dev_encode(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None):
         _check(lib().ans_dev_encode_chunks(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, _dptr(d_slots), slot_cap,
@@ -785,6 +820,60 @@ class GpuDenseSet:
             _check(rc, "ans_gpu_dense_set_decode")
             return edges[:count.value]
         raise AnsError(ANS_E_LEN, "ans_gpu_dense_set_decode")
+
+
+class GpuDenseSets:
+    """A dataset of graphs under one ErdosRenyi Bernoulli (GraphDatasetParamCodec with
+    ErdosRenyiParamCodec, src/param_codec.rs:171-199,243-293) on the GPU: graph g is one
+    message (one chunk of the variable-chunk path)."""
+
+    def __init__(self, gpu, edge, directed=False, loops=False):
+        self.gpu = gpu
+        self.edge = edge
+        self.table = GpuTable(gpu, edge.categorical)
+        self.directed, self.loops = int(bool(directed)), int(bool(loops))
+
+    def encode(self, num_nodes, edge_lists):
+        """num_nodes: per graph; edge_lists: per graph an (m_g, 2) array.  Returns
+        (bytes, offsets, lens), one stream per graph."""
+        nn = np.ascontiguousarray(np.asarray(num_nodes, dtype=np.uint32))
+        parts = [np.asarray(e, dtype=np.uint32).reshape(-1, 2) for e in edge_lists]
+        eo = np.zeros(len(parts) + 1, np.uint64)
+        eo[1:] = np.cumsum([len(p) for p in parts])
+        edges = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros((0, 2), np.uint32))
+        sizes = [len(AllEdgeIndices(int(n), self.directed, self.loops)) for n in nn]
+        cap = sum(self.table.slot_capacity(max(sizes) if sizes else 0) for _ in sizes)
+        out = np.empty(max(cap, 1), np.uint8)
+        offsets = np.zeros(max(len(nn), 1), np.uint64)
+        lens = np.zeros(max(len(nn), 1), np.uint64)
+        total = u64(0)
+        _check(lib().ans_gpu_dense_sets_encode(self.table.h, len(nn), _np_ptr(nn), self.directed, self.loops,
+                                               _np_ptr(edges), _np_ptr(eo), _np_ptr(out), len(out), _np_ptr(offsets),
+                                               _np_ptr(lens), ctypes.byref(total)), "ans_gpu_dense_sets_encode")
+        return out[:total.value], offsets[:len(nn)], lens[:len(nn)]
+
+    def decode(self, num_nodes, data, offsets, lens, cap=None):
+        """Returns the per-graph edge arrays (alphabet order)."""
+        nn = np.ascontiguousarray(np.asarray(num_nodes, dtype=np.uint32))
+        data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+        offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        slots = sum(len(AllEdgeIndices(int(n), self.directed, self.loops)) for n in nn)
+        if cap is None:
+            cap = int(2 * self.edge.prob() * slots) + 1024
+        cap = min(cap, slots)
+        eo = np.zeros(len(nn) + 1, np.uint64)
+        for _ in range(2):
+            edges = np.zeros((max(cap, 1), 2), np.uint32)
+            rc = lib().ans_gpu_dense_sets_decode(self.table.h, len(nn), _np_ptr(nn), self.directed, self.loops,
+                                                 _np_ptr(data) if data.size else None, data.size, _np_ptr(offsets),
+                                                 _np_ptr(lens), _np_ptr(edges), cap, _np_ptr(eo))
+            if rc == ANS_E_LEN and int(eo[-1]) > cap:
+                cap = int(eo[-1])
+                continue
+            _check(rc, "ans_gpu_dense_sets_decode")
+            return [edges[int(eo[g]):int(eo[g + 1])] for g in range(len(nn))]
+        raise AnsError(ANS_E_LEN, "ans_gpu_dense_sets_decode")
 
 
 # ============================================================== synthetic tables (SURVEY.md §8d)

@@ -69,3 +69,9 @@ struct ans_gpu_table {
             return ANS_E_DEVICE;                                                                       \
         }                                                                                              \
     } while (0)
+
+// Variable-chunk encode of device-resident symbols into a host container (ans_kernels.hip):
+// the body of ans_gpu_encode_var_chunks; starts is a host array of nchunks + 1 entries.
+int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                               const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
+                               uint64_t* lens, uint64_t* total);

@@ -178,6 +178,98 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_emit(EdgeSpace es, const 
     }
 }
 
+// ---- datasets of graphs: graph g's alphabet occupies slots [S[g], S[g+1]) of one dense vector
+
+// index of the graph holding position x: the last g with bounds[g] <= x (bounds non-decreasing)
+__device__ inline uint64_t graph_of(const uint64_t* bounds, uint64_t num_graphs, uint64_t x) {
+    uint64_t lo = 0, hi = num_graphs;  // bounds[lo] <= x < bounds[hi]
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (bounds[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// one lane per edge: its graph from the edge offsets, its slot inside that graph's alphabet
+__global__ __launch_bounds__(256) void k_edges_to_dense_multi(uint32_t directed, uint32_t loops,
+                                                              const uint32_t* __restrict__ num_nodes,
+                                                              const uint64_t* __restrict__ S,
+                                                              const uint64_t* __restrict__ edge_offsets,
+                                                              uint64_t num_graphs, const uint32_t* __restrict__ edges,
+                                                              uint64_t m, uint8_t* __restrict__ dense,
+                                                              uint32_t* __restrict__ status) {
+    const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t g = graph_of(edge_offsets, num_graphs, k);
+    const EdgeSpace e{num_nodes[g], directed, loops};
+    const uint64_t s = edge_slot(e, edges[2 * k], edges[2 * k + 1]);
+    if (s == ~0ull) {
+        atomicOr(status, 1u << ANS_E_SYMBOL);
+        return;
+    }
+    dense[S[g] + s] = 1;
+}
+
+// pass 3 for datasets: like k_tile_emit, each set slot mapped to (graph, local slot) first
+__global__ __launch_bounds__(kTileThreads) void k_tile_emit_multi(uint32_t directed, uint32_t loops,
+                                                                  const uint32_t* __restrict__ num_nodes,
+                                                                  const uint64_t* __restrict__ S, uint64_t num_graphs,
+                                                                  const uint8_t* __restrict__ dense, uint64_t len,
+                                                                  const uint64_t* __restrict__ base,
+                                                                  uint32_t* __restrict__ edges, uint64_t cap,
+                                                                  uint32_t* __restrict__ status) {
+    __shared__ uint32_t wsum[kTileThreads / 64];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x / 64;
+    const uint64_t pos = blockIdx.x * kTileSlots + 16ull * threadIdx.x;
+    const uint4 v = pos < len ? load_tile_word(dense, len, pos) : make_uint4(0, 0, 0, 0);
+    const uint32_t c = count16(v);
+    uint32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if (lane >= static_cast<uint32_t>(d)) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < wave; ++w) carry += wsum[w];
+    if (c == 0) return;
+    uint64_t out = base[blockIdx.x] + carry + incl - c;
+    const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+    for (int b = 0; b < 16; ++b) {
+        if (((words[b / 4] >> (8 * (b % 4))) & 0xFFu) == 0) continue;
+        if (out >= cap) {
+            atomicOr(status, 1u << ANS_E_LEN);
+            return;
+        }
+        const uint64_t x = pos + b;
+        const uint64_t g = graph_of(S, num_graphs, x);
+        uint32_t i, j;
+        slot_edge(EdgeSpace{num_nodes[g], directed, loops}, x - S[g], i, j);
+        edges[2 * out] = i;
+        edges[2 * out + 1] = j;
+        ++out;
+    }
+}
+
+// per graph: set slots before S[g] (tile base + the partial tile), i.e. graph g's first edge
+__global__ __launch_bounds__(256) void k_graph_edge_offsets(const uint8_t* __restrict__ dense,
+                                                            const uint64_t* __restrict__ S, uint64_t num_graphs,
+                                                            const uint64_t* __restrict__ base,
+                                                            const uint64_t* __restrict__ total,
+                                                            uint64_t* __restrict__ edge_offsets) {
+    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (g > num_graphs) return;
+    if (g == num_graphs) {
+        edge_offsets[g] = *total;
+        return;
+    }
+    const uint64_t x = S[g], tile = x / kTileSlots;
+    uint64_t cnt = base[tile];
+    for (uint64_t y = tile * kTileSlots; y < x; ++y) cnt += dense[y] != 0;
+    edge_offsets[g] = cnt;
+}
+
 inline unsigned blocks_for(uint64_t lanes, unsigned per) { return static_cast<unsigned>((lanes + per - 1) / per); }
 
 int scratch(ans_gpu* g, size_t bytes, void** out) {
@@ -371,6 +463,128 @@ int ans_gpu_dense_set_decode(ans_gpu_table* gt, uint64_t num_nodes, int directed
     HIP_TRY(hipMemcpy(&count, d_count.p, 8, hipMemcpyDeviceToHost));
     *num_edges = count;
     if (st && st != ANS_E_LEN) return st;
+    const uint64_t got = std::min(count, cap);
+    if (got) HIP_TRY(hipMemcpy(edges, d_edges.p, 8 * got, hipMemcpyDeviceToHost));
+    return count > cap ? ANS_E_LEN : ANS_OK;
+}
+
+// Independent<GraphIID<ErdosRenyi>> over a dataset (GraphDatasetParamCodec, src/param_codec.rs:
+// 243-293, whose ErdosRenyiParamCodec gives every graph the same Bernoulli, src/param_codec.rs:
+// 171-199; DatasetStats::unlabelled, src/benchmark.rs:552-557): graph g is one chunk of the
+// variable-chunk path, its stream the reference message of that graph's edge set.
+static int dataset_space(uint64_t num_graphs, const uint32_t* num_nodes, int directed, int loops,
+                         std::vector<uint64_t>& S) {
+    S.assign(num_graphs + 1, 0);
+    for (uint64_t g = 0; g < num_graphs; ++g)
+        S[g + 1] = S[g] + alphabet_len(EdgeSpace{num_nodes[g], directed ? 1u : 0u, loops ? 1u : 0u});
+    return ANS_OK;
+}
+
+int ans_gpu_dense_sets_encode(ans_gpu_table* gt, uint64_t num_graphs, const uint32_t* num_nodes, int directed,
+                              int loops, const uint32_t* edges, const uint64_t* edge_offsets, uint8_t* out,
+                              uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !total || (num_graphs && (!num_nodes || !edge_offsets))) return ANS_E_ARG;
+    if (gt->t.nsym != 2) return ANS_E_ARG;
+    *total = 0;
+    if (num_graphs == 0) return ANS_OK;
+    for (uint64_t g = 0; g < num_graphs; ++g)
+        if (edge_offsets[g + 1] < edge_offsets[g]) return ANS_E_ARG;
+    const uint64_t m = edge_offsets[num_graphs] - edge_offsets[0];
+    if (m && !edges) return ANS_E_ARG;
+    std::vector<uint64_t> S;
+    dataset_space(num_graphs, num_nodes, directed, loops, S);
+    ans_gpu* gp = gt->g;
+    HIP_TRY(hipSetDevice(gp->device));
+    const hipStream_t s = gp->stream;
+    std::vector<uint64_t> eo(edge_offsets, edge_offsets + num_graphs + 1);
+    for (auto& v : eo) v -= edge_offsets[0];
+    Buf d_dense, d_edges, d_nn, d_S, d_eo, d_status;
+    if (!d_dense.alloc(S[num_graphs] + 16) || !d_edges.alloc(8 * m) || !d_nn.alloc(4 * num_graphs) ||
+        !d_S.alloc(8 * (num_graphs + 1)) || !d_eo.alloc(8 * (num_graphs + 1)) || !d_status.alloc(16))
+        return ANS_E_DEVICE;
+    if (m) HIP_TRY(hipMemcpyAsync(d_edges.p, edges + 2 * edge_offsets[0], 8 * m, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_nn.p, num_nodes, 4 * num_graphs, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_S.p, S.data(), 8 * (num_graphs + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_eo.p, eo.data(), 8 * (num_graphs + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
+    if (S[num_graphs]) HIP_TRY(hipMemsetAsync(d_dense.p, 0, S[num_graphs], s));
+    if (m) {
+        k_edges_to_dense_multi<<<blocks_for(m, 256), 256, 0, s>>>(directed ? 1u : 0u, loops ? 1u : 0u,
+                                                                  d_nn.as<uint32_t>(), d_S.as<uint64_t>(),
+                                                                  d_eo.as<uint64_t>(), num_graphs,
+                                                                  d_edges.as<uint32_t>(), m, d_dense.as<uint8_t>(),
+                                                                  d_status.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+    }
+    int st = 0;
+    int rc = ans_dev_status(gp, d_status.as<uint32_t>(), s, &st);
+    if (rc) return rc;
+    if (st) return st;
+    return ans_encode_var_from_device(gt, d_dense.p, 1, num_graphs, S.data(), out, out_cap, offsets, lens, total);
+}
+
+int ans_gpu_dense_sets_decode(ans_gpu_table* gt, uint64_t num_graphs, const uint32_t* num_nodes, int directed,
+                              int loops, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                              const uint64_t* lens, uint32_t* edges, uint64_t cap, uint64_t* edge_offsets) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !edge_offsets || (num_graphs && (!num_nodes || !offsets || !lens)) || (cap && !edges))
+        return ANS_E_ARG;
+    if (gt->t.nsym != 2) return ANS_E_ARG;
+    edge_offsets[0] = 0;
+    if (num_graphs == 0) return ANS_OK;
+    std::vector<uint64_t> S;
+    dataset_space(num_graphs, num_nodes, directed, loops, S);
+    std::vector<uint32_t> l32(num_graphs);
+    for (uint64_t g = 0; g < num_graphs; ++g) {
+        if (lens[g] > 0xffffffffull || offsets[g] > in_len || lens[g] > in_len - offsets[g]) return ANS_E_LEN;
+        l32[g] = static_cast<uint32_t>(lens[g]);
+    }
+    if (in_len && !in) return ANS_E_ARG;
+    const uint64_t len = S[num_graphs];
+    ans_gpu* gp = gt->g;
+    HIP_TRY(hipSetDevice(gp->device));
+    const hipStream_t s = gp->stream;
+    const uint64_t ntiles = (len + kTileSlots - 1) / kTileSlots;
+    Buf d_in, d_offs, d_lens, d_S, d_nn, d_dense, d_status, d_edges, d_scan, d_eo;
+    if (!d_in.alloc(in_len + 16) || !d_offs.alloc(8 * num_graphs) || !d_lens.alloc(4 * num_graphs) ||
+        !d_S.alloc(8 * (num_graphs + 1)) || !d_nn.alloc(4 * num_graphs) || !d_dense.alloc(len + 16) ||
+        !d_status.alloc(16) || !d_edges.alloc(8 * cap) || !d_scan.alloc(12 * ntiles + 16) ||
+        !d_eo.alloc(8 * (num_graphs + 1)))
+        return ANS_E_DEVICE;
+    if (in_len) HIP_TRY(hipMemcpyAsync(d_in.p, in, in_len, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_offs.p, offsets, 8 * num_graphs, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_lens.p, l32.data(), 4 * num_graphs, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_S.p, S.data(), 8 * (num_graphs + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_nn.p, num_nodes, 4 * num_graphs, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_status.p, 0, 16, s));
+    int rc = ans_dev_decode_var_chunks(gt, d_in.as<uint8_t>(), d_offs.as<uint64_t>(), 0, d_lens.as<uint32_t>(),
+                                       num_graphs, d_S.as<uint64_t>(), ANS_GEN_ZEROS, d_dense.p, 1,
+                                       d_status.as<uint32_t>(), s);
+    if (rc) return rc;
+    auto* base = d_scan.as<uint64_t>();
+    auto* counts = reinterpret_cast<uint32_t*>(base + ntiles);
+    uint64_t* d_total = d_status.as<uint64_t>() + 1;  // second 8 bytes of the status block
+    if (ntiles) {
+        k_tile_count<<<static_cast<unsigned>(ntiles), kTileThreads, 0, s>>>(d_dense.as<uint8_t>(), len, counts);
+        HIP_TRY(hipGetLastError());
+        k_tile_scan<<<1, 1024, 0, s>>>(counts, ntiles, base, d_total);
+        HIP_TRY(hipGetLastError());
+        k_tile_emit_multi<<<static_cast<unsigned>(ntiles), kTileThreads, 0, s>>>(
+            directed ? 1u : 0u, loops ? 1u : 0u, d_nn.as<uint32_t>(), d_S.as<uint64_t>(), num_graphs,
+            d_dense.as<uint8_t>(), len, base, d_edges.as<uint32_t>(), cap, d_status.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+        k_graph_edge_offsets<<<blocks_for(num_graphs + 1, 256), 256, 0, s>>>(d_dense.as<uint8_t>(), d_S.as<uint64_t>(),
+                                                                           num_graphs, base, d_total,
+                                                                           d_eo.as<uint64_t>());
+        HIP_TRY(hipGetLastError());
+    }
+    int st = 0;
+    if ((rc = ans_dev_status(gp, d_status.as<uint32_t>(), s, &st))) return rc;
+    if (st && st != ANS_E_LEN) return st;
+    if (ntiles) HIP_TRY(hipMemcpy(edge_offsets, d_eo.p, 8 * (num_graphs + 1), hipMemcpyDeviceToHost));
+    else std::fill(edge_offsets, edge_offsets + num_graphs + 1, 0);
+    const uint64_t count = edge_offsets[num_graphs];
     const uint64_t got = std::min(count, cap);
     if (got) HIP_TRY(hipMemcpy(edges, d_edges.p, 8 * got, hipMemcpyDeviceToHost));
     return count > cap ? ANS_E_LEN : ANS_OK;

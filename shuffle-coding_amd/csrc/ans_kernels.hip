@@ -131,7 +131,8 @@ struct ByteSource {
 // Encode: lane = chunk; symbols consumed last -> first (IID::push, src/codec.rs:417).
 template <typename Sym, bool kLds, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __restrict__ syms, uint64_t n,
-                                                   uint64_t chunk_len, uint64_t c_first, uint64_t nchunks,
+                                                   uint64_t chunk_len, const uint64_t* __restrict__ starts,
+                                                   uint64_t c_first, uint64_t nchunks,
                                                    uint8_t* __restrict__ slots,
                                                    uint64_t slot_cap, uint32_t* __restrict__ lens,
                                                    uint32_t* __restrict__ status) {
@@ -143,8 +144,9 @@ __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __rest
     }
     const uint64_t c = c_first + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (c >= nchunks) return;
-    const uint64_t a = c * chunk_len;
-    const uint64_t b = min(a + chunk_len, n);
+    // chunk c: fixed-length [c*L, min(n, (c+1)*L)), or [starts[c], starts[c+1]) (variable chunks)
+    const uint64_t a = starts ? starts[c] : c * chunk_len;
+    const uint64_t b = starts ? starts[c + 1] : min(a + chunk_len, n);
     ByteSink sink{slots + c * slot_cap, slot_cap, 0, 0, 0, false};
     uint64_t head = kMaxMinHead;  // Message::zeros()
     const uint64_t norm = t.norm, K = t.K;
@@ -191,6 +193,7 @@ template <typename Sym, bool kLds, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ offsets, uint64_t slot_cap,
                                                    const uint32_t* __restrict__ lens, uint64_t n, uint64_t chunk_len,
+                                                   const uint64_t* __restrict__ starts,
                                                    uint64_t c_first, uint64_t nchunks, int gen_kind, Sym* __restrict__ out,
                                                    uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
@@ -203,8 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
     }
     const uint64_t c = c_first + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (c >= nchunks) return;
-    const uint64_t a = c * chunk_len;
-    const uint64_t b = min(a + chunk_len, n);
+    const uint64_t a = starts ? starts[c] : c * chunk_len;
+    const uint64_t b = starts ? starts[c + 1] : min(a + chunk_len, n);
     ByteSource src;
     src.init(in + (offsets ? offsets[c] : c * slot_cap), lens[c]);
     uint64_t head = 0;  // Message::unflatten
@@ -480,13 +483,13 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     const unsigned grid = grid_for(nchunks - nfull);
     const size_t lds = gt->lds_bytes ? sizeof(DevSym) * (t.nsym + 1) : 0;
     if (gt->lds_bytes && t.fast)
-        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     else if (gt->lds_bytes)
-        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     else if (t.fast)
-        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     else
-        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -530,13 +533,13 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const unsigned grid = grid_for(nchunks - nfull);
     const size_t lds = gt->lds_bytes;
     if (gt->lds_bytes && t.fast)
-        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
     else if (gt->lds_bytes)
-        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
     else if (t.fast)
-        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
     else
-        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -550,6 +553,49 @@ int launch_gen(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, voi
         k_gen_iid<Sym, true><<<grid, kBlock, gt->lds_bytes, s>>>(gt->t, seed, start, n, static_cast<Sym*>(d_syms));
     else
         k_gen_iid<Sym, false><<<grid, kBlock, 0, s>>>(gt->t, seed, start, n, static_cast<Sym*>(d_syms));
+    HIP_TRY(hipGetLastError());
+    return ANS_OK;
+}
+
+// Variable-length chunks (chunk c = symbols [d_starts[c], d_starts[c+1])): generic kernels,
+// one lane per chunk, slots of slot_cap bytes.
+template <typename Sym>
+int launch_encode_var(ans_gpu_table* gt, const void* d_syms, uint64_t nchunks, const uint64_t* d_starts,
+                      uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s) {
+    if (nchunks == 0) return ANS_OK;
+    const DevTable& t = gt->t;
+    const Sym* syms = static_cast<const Sym*>(d_syms);
+    const unsigned grid = grid_for(nchunks);
+    const size_t lds = gt->lds_bytes ? sizeof(DevSym) * (t.nsym + 1) : 0;
+    if (gt->lds_bytes && t.fast)
+        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+    else if (gt->lds_bytes)
+        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+    else if (t.fast)
+        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+    else
+        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+    HIP_TRY(hipGetLastError());
+    return ANS_OK;
+}
+
+template <typename Sym>
+int launch_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                      const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind, void* d_syms,
+                      uint32_t* d_status, hipStream_t s) {
+    if (nchunks == 0) return ANS_OK;
+    const DevTable& t = gt->t;
+    Sym* out = static_cast<Sym*>(d_syms);
+    const unsigned grid = grid_for(nchunks);
+    const size_t lds = gt->lds_bytes;
+    if (gt->lds_bytes && t.fast)
+        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+    else if (gt->lds_bytes)
+        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+    else if (t.fast)
+        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+    else
+        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -1267,6 +1313,61 @@ int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t*
 
 }  // namespace
 
+// Variable-chunk encode of symbols already on the device (ans_ctx.hpp): the body of
+// ans_gpu_encode_var_chunks, also used by the graph dataset coder (ans_graph.hip).
+int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                               const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
+                               uint64_t* lens, uint64_t* total) {
+    if (out && nchunks && (!offsets || !lens)) return ANS_E_ARG;
+    *total = 0;
+    if (nchunks == 0) return ANS_OK;
+    uint64_t maxlen = 0;
+    for (uint64_t c = 0; c < nchunks; ++c) maxlen = std::max(maxlen, starts[c + 1] - starts[c]);
+    uint64_t slot_cap = 0;
+    ans_gpu_slot_capacity(gt, maxlen, &slot_cap);
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = gt->g->stream;
+    DevBuf d_starts, d_slots, d_lens, d_status, d_offs, d_out;
+    HIP_TRY(d_starts.alloc(8 * (nchunks + 1)));
+    HIP_TRY(d_slots.alloc(nchunks * slot_cap));
+    HIP_TRY(d_lens.alloc(4 * nchunks));
+    HIP_TRY(d_status.alloc(4));
+    HIP_TRY(hipMemcpyAsync(d_starts.p, starts, 8 * (nchunks + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
+    int rc = ans_dev_encode_var_chunks(gt, d_syms, sym_bytes, nchunks, static_cast<uint64_t*>(d_starts.p),
+                                       static_cast<uint8_t*>(d_slots.p), slot_cap, static_cast<uint32_t*>(d_lens.p),
+                                       static_cast<uint32_t*>(d_status.p), s);
+    if (rc) return rc;
+    int st = 0;
+    if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
+    if (st) return st;
+    std::vector<uint32_t> hl(nchunks);
+    HIP_TRY(hipMemcpy(hl.data(), d_lens.p, 4 * nchunks, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> off(nchunks);
+    uint64_t acc = 0;
+    for (uint64_t c = 0; c < nchunks; ++c) {
+        off[c] = acc;
+        acc += hl[c];
+    }
+    *total = acc;
+    if (!out) return ANS_OK;
+    if (out_cap < acc) return ANS_E_LEN;
+    for (uint64_t c = 0; c < nchunks; ++c) {
+        offsets[c] = off[c];
+        lens[c] = hl[c];
+    }
+    if (!acc) return ANS_OK;
+    HIP_TRY(d_offs.alloc(8 * nchunks));
+    HIP_TRY(d_out.alloc(acc));
+    HIP_TRY(hipMemcpyAsync(d_offs.p, off.data(), 8 * nchunks, hipMemcpyHostToDevice, s));
+    if ((rc = ans_dev_compact(gt->g, static_cast<uint8_t*>(d_slots.p), slot_cap, static_cast<uint32_t*>(d_lens.p),
+                              static_cast<uint64_t*>(d_offs.p), nchunks, static_cast<uint8_t*>(d_out.p), s)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(out, d_out.p, acc, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return ANS_OK;
+}
+
 // ====================================================================== C ABI (GPU part)
 extern "C" {
 
@@ -1479,6 +1580,95 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
     if (rc) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(out, d.p, n * sym_bytes, hipMemcpyDeviceToHost, gt->g->stream));
     HIP_TRY(hipStreamSynchronize(gt->g->stream));
+    return ANS_OK;
+}
+
+int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                              const uint64_t* d_starts, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
+                              uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !d_status || !valid_width(sym_bytes) || (slot_cap & 15)) return ANS_E_ARG;
+    if (nchunks && (!d_syms || !d_starts || !d_slots || !d_lens)) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = pick(gt, stream);
+    switch (sym_bytes) {
+    case 1: return launch_encode_var<uint8_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s);
+    case 2: return launch_encode_var<uint16_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s);
+    default: return launch_encode_var<uint32_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s);
+    }
+}
+
+int ans_dev_decode_var_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                              const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
+                              void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !d_status || !valid_width(sym_bytes)) return ANS_E_ARG;
+    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;
+    if (nchunks && (!d_in || !d_lens || !d_starts || !d_syms)) return ANS_E_ARG;
+    if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = pick(gt, stream);
+    switch (sym_bytes) {
+    case 1: return launch_decode_var<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s);
+    case 2: return launch_decode_var<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s);
+    default: return launch_decode_var<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s);
+    }
+}
+
+int ans_gpu_encode_var_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t nchunks,
+                              const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
+                              uint64_t* lens, uint64_t* total) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !valid_width(sym_bytes) || !total || (nchunks && !starts)) return ANS_E_ARG;
+    *total = 0;
+    if (nchunks == 0) return ANS_OK;
+    for (uint64_t c = 0; c < nchunks; ++c)
+        if (starts[c + 1] < starts[c]) return ANS_E_ARG;
+    const uint64_t n = starts[nchunks];
+    if (n && !syms) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    DevBuf d_syms;
+    HIP_TRY(d_syms.alloc(n * sym_bytes));
+    if (n) HIP_TRY(hipMemcpyAsync(d_syms.p, syms, n * sym_bytes, hipMemcpyHostToDevice, gt->g->stream));
+    return ans_encode_var_from_device(gt, d_syms.p, sym_bytes, nchunks, starts, out, out_cap, offsets, lens, total);
+}
+
+int ans_gpu_decode_var_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                              const uint64_t* lens, uint64_t nchunks, const uint64_t* starts, int gen_kind, void* out,
+                              int sym_bytes) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !valid_width(sym_bytes) || (nchunks && (!starts || !offsets || !lens))) return ANS_E_ARG;
+    if (nchunks == 0) return ANS_OK;
+    std::vector<uint32_t> l32(nchunks);
+    for (uint64_t c = 0; c < nchunks; ++c) {
+        if (starts[c + 1] < starts[c]) return ANS_E_ARG;
+        if (lens[c] > 0xffffffffull || offsets[c] > in_len || lens[c] > in_len - offsets[c]) return ANS_E_LEN;
+        l32[c] = static_cast<uint32_t>(lens[c]);
+    }
+    const uint64_t n = starts[nchunks];
+    if ((n && !out) || (in_len && !in)) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = gt->g->stream;
+    DevBuf d_in, d_offs, d_lens, d_starts, d_out, d_status;
+    HIP_TRY(d_in.alloc(in_len + 16));
+    HIP_TRY(d_offs.alloc(8 * nchunks));
+    HIP_TRY(d_lens.alloc(4 * nchunks));
+    HIP_TRY(d_starts.alloc(8 * (nchunks + 1)));
+    HIP_TRY(d_out.alloc(n * sym_bytes));
+    HIP_TRY(d_status.alloc(4));
+    if (in_len) HIP_TRY(hipMemcpyAsync(d_in.p, in, in_len, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_offs.p, offsets, 8 * nchunks, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_lens.p, l32.data(), 4 * nchunks, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_starts.p, starts, 8 * (nchunks + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
+    int rc = ans_dev_decode_var_chunks(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_offs.p), 0,
+                                       static_cast<uint32_t*>(d_lens.p), nchunks, static_cast<uint64_t*>(d_starts.p),
+                                       gen_kind, d_out.p, sym_bytes, static_cast<uint32_t*>(d_status.p), s);
+    if (rc) return rc;
+    int st = 0;
+    if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
+    if (st) return st;
+    if (n) HIP_TRY(hipMemcpy(out, d_out.p, n * sym_bytes, hipMemcpyDeviceToHost));
     return ANS_OK;
 }
 

@@ -499,3 +499,30 @@ def test_boundary_tables_bit_exact(gpu, name):
     # uniform over the symbols, so the rare (tiny-mass) symbols are coded often
     syms = rng.choice(nz, size=520 * 4096 + 77).astype(np.uint32)
     _roundtrip_vs_oracle(gpu, masses, syms, 4096, np.uint8 if len(masses) <= 256 else np.uint16)
+
+
+# ---------------------------------------------------------------- variable-length chunks
+@pytest.mark.parametrize("which", ["c3", "multiset", "tiny_norm"])
+def test_var_chunks_bit_exact(gpu, which, multiset_masses):
+    """Chunk c = syms[starts[c]:starts[c+1]] (empty, one-symbol and long chunks mixed): each
+    stream is the reference message of that slice alone (one oracle message per chunk)."""
+    rng = np.random.default_rng(31)
+    masses = {"c3": A.c3_masses(), "multiset": multiset_masses,
+              "tiny_norm": np.asarray([3, 0, 5, 1, 7], np.uint64)}[which]
+    sizes = np.concatenate([[0, 1, 0, 7], rng.integers(0, 3000, 300), [20000, 0]]).astype(np.uint64)
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    n = int(starts[-1])
+    nz = np.flatnonzero(masses)
+    p = masses[nz].astype(np.float64)
+    syms = rng.choice(nz, size=n, p=p / p.sum()).astype(np.uint32)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    dtype = np.uint16 if len(masses) > 256 else np.uint8
+    data, offsets, lens = gt.encode_var_chunks(syms.astype(dtype), starts)
+    for c in range(len(sizes)):
+        a, b = int(starts[c]), int(starts[c + 1])
+        od, _, ol = orc.encode_chunks(masses, syms[a:b], max(b - a, 1))
+        want = od.tobytes() if b > a else bytes(orc.Message.zeros().flatten())
+        got = data[int(offsets[c]):int(offsets[c] + lens[c])].tobytes()
+        assert got == want, c
+    back = gt.decode_var_chunks(data, offsets, lens, starts, dtype)
+    assert np.array_equal(back, syms.astype(dtype))

@@ -141,3 +141,31 @@ def test_gpu_dense_set_edge_cases():
         z = A.GpuDenseSet(g, A.Bernoulli(mass, NORM), n)
         data, offsets, lens = z.encode(np.zeros((0, 2), np.uint32), 64)
         assert len(data) == 0 and len(z.decode(data, offsets, lens, 64)) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("directed,loops", [(False, False), (True, True)])
+def test_gpu_graph_dataset_bit_exact(directed, loops):
+    """A dataset under one Bernoulli (GraphDatasetParamCodec + ErdosRenyiParamCodec,
+    src/param_codec.rs:171-199,243-293): graph g's stream is the reference message of that
+    graph's edge set alone; decoding returns every graph's edges in alphabet order."""
+    rng = np.random.default_rng(11 + directed)
+    nums = [int(x) for x in rng.integers(0, 60, 80)] + [0, 1, 2, 150]
+    p = 0.08
+    masses, mass = _er_masses(p)
+    graphs = [_random_graph(rng, n, p, directed, loops) for n in nums]
+    ds = A.GpuDenseSets(A.Gpu(0), A.Bernoulli(mass, NORM), directed, loops)
+    data, offsets, lens = ds.encode(nums, graphs)
+    for g, (n, e) in enumerate(zip(nums, graphs)):
+        er = A.ErdosRenyi(A.Bernoulli(mass, NORM), n, directed, loops)
+        m = A.Message.zeros()
+        er.push(m, [tuple(map(int, x)) for x in e])
+        assert data[int(offsets[g]):int(offsets[g] + lens[g])].tobytes() == m.flatten(), g
+    back = ds.decode(nums, data, offsets, lens, cap=5)  # too small: the second pass sizes it
+    for g, (n, e) in enumerate(zip(nums, graphs)):
+        want = _alphabet_sorted(e, n, directed, loops) if len(e) else np.zeros((0, 2), np.uint32)
+        assert np.array_equal(back[g], want), g
+    bad = [np.asarray([[3, 1]], np.uint32) if not directed else np.asarray([[70, 1]], np.uint32)] + graphs[1:]
+    with pytest.raises(A.AnsError) as e:
+        ds.encode(nums, bad)
+    assert e.value.code == A.ANS_E_SYMBOL
