@@ -35,7 +35,7 @@ constexpr uint32_t kEncMcOffset = 8 * 257;  // encode LDS: rcp[257], (mass, cum)
 constexpr uint32_t kEncPkOffset = 2 * kEncMcOffset;
 constexpr uint32_t kEncLdsBytes = (3 * kEncMcOffset + 15) & ~15u;
 constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB at LDS offset 0
-constexpr uint32_t kDecTableBytes = 14336;  // decode buckets in LDS: 2 x (66 KiB ring + 14 KiB) per CU
+constexpr uint32_t kDecTableBytes = 28672;  // decode buckets + cdf in LDS beside the 132 KiB ring (k_decode)
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // Non-temporal 16-byte global load / store (streamed data that must not evict cached tables).
@@ -389,8 +389,14 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
 // below `low` is always in flight in registers (S); pages below 0 are zeros (the Zeros
 // generator, src/ans.rs:160-170).  A point covers at most 60 stream bytes (SPP symbols of at
 // most KMAX bytes), so no read between points can reach an unlanded page.
+// The decoder runs 1,024-lane workgroups, one per CU: the lanes share ONE copy of the tables,
+// so the whole 160 KiB of LDS holds the 1,024 rings (132 KiB) plus 28 KiB of tables, twice the
+// table room two 512-lane workgroups would leave (finer icdf buckets: C3 resolves every cf with
+// three candidates and compiles no far path).
+constexpr int kDecBlock = 1024;
 constexpr int kDecRows = 33;
-constexpr uint32_t kDecRingBytes = kDecRows * kBlock * 4;
+constexpr uint32_t kDecRingBytes = kDecRows * kDecBlock * 4;
+static_assert(kDecRingBytes + kDecTableBytes == 160 * 1024, "decode LDS = one CU's 160 KiB");
 
 struct DecChain {
     uint32_t* ring;  // &ring[0][lane]
@@ -404,7 +410,7 @@ struct DecChain {
     uint32_t cf, cum, nxt, sx;
     bool far;
 
-    __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kBlock]; }
+    __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kDecBlock]; }
     __device__ __forceinline__ void put_page(int32_t p) {
         const int32_t r0 = (p & 1) * 16;
 #pragma unroll
@@ -427,12 +433,12 @@ struct DecChain {
         }
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
-    // ring at LDS offset 0 the row address is one v_and_or of (P << 9) and the lane's column.
+    // ring at LDS offset 0 the row address is one v_and_or of (P << 10) and the lane's column.
     uint32_t wx, wy, col;  // col = 4 * lane: the lane's byte column in the ring (LDS offset 0)
     __device__ __forceinline__ void read_window() {
-        const uint32_t a = ((static_cast<uint32_t>(P) << 9) & 0xF800u) | col;  // row (P>>2)&31
+        const uint32_t a = ((static_cast<uint32_t>(P) << 10) & 0x1F000u) | col;  // row (P>>2)&31
         wy = lds_ld32(a);
-        wx = lds_ld32(a + 4 * kBlock);
+        wx = lds_ld32(a + 4 * kDecBlock);
     }
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P) & 3u); }
     // the top two pages land before decoding starts; the third is requested
@@ -523,7 +529,7 @@ struct DecChain {
 // kFar: some bucket holds more than four cdf boundaries, so the voted slow path is compiled in.
 // kP24: every mass is below 2^24 (DecChain::update).
 template <typename Sym, int SPP, bool kFar, bool kP24>
-__global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
+__global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
                                                       uint32_t* __restrict__ status) {
@@ -532,13 +538,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_decode(FastTable t, const uint8_t
     {
         uint4* b = reinterpret_cast<uint4*>(tab);  // buckets and s0 array: dec_cum_off bytes
         const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt);
-        for (uint32_t i = threadIdx.x; i < t.dec_cum_off / 16; i += kBlock) b[i] = gb[i];
+        for (uint32_t i = threadIdx.x; i < t.dec_cum_off / 16; i += kDecBlock) b[i] = gb[i];
         uint32_t* cl = reinterpret_cast<uint32_t*>(tab + t.dec_cum_off);
-        for (uint32_t i = threadIdx.x; i < t.nsym + 5; i += kBlock) cl[i] = t.cum[i];
+        for (uint32_t i = threadIdx.x; i < t.nsym + 5; i += kDecBlock) cl[i] = t.cum[i];
     }
     const uint32_t* lcum = reinterpret_cast<const uint32_t*>(tab + t.dec_cum_off);
     __syncthreads();
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kDecBlock + threadIdx.x;
     if (c >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));

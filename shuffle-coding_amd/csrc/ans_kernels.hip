@@ -517,7 +517,8 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
                 fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
-#define DEC(SPP, FAR, P24) fast::k_decode<Sym, SPP, FAR, P24><<<grid, fast::kBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
+            const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
+#define DEC(SPP, FAR, P24) fast::k_decode<Sym, SPP, FAR, P24><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
 #define DEC_P(SPP, FAR) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true); else DEC(SPP, FAR, false)
             if (U * ft.kmax > 60) {
                 if (ft.dec_far) { DEC_P(U / 2, true); } else { DEC_P(U / 2, false); }
