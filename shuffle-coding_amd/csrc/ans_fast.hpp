@@ -31,9 +31,11 @@ namespace fast {
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
-constexpr uint32_t kEncMcOffset = 8 * 257;  // encode LDS: rcp[257], (mass, cum)[257], p*K[257]
-constexpr uint32_t kEncPkOffset = 2 * kEncMcOffset;
-constexpr uint32_t kEncLdsBytes = (3 * kEncMcOffset + 15) & ~15u;
+// encode LDS after the ring: rcp[257], (mass, cum)[257], then the renorm thresholds
+// thr_j[257] = p*K*2^(8j) - 1 (saturated), j = 1..KMAX (at most 4)
+constexpr uint32_t kEncMcOffset = 8 * 257;
+constexpr uint32_t kEncThrOffset = 2 * kEncMcOffset;
+constexpr uint32_t kEncLdsBytes = (6 * kEncMcOffset + 15) & ~15u;
 constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB at LDS offset 0
 constexpr uint32_t kDecTableBytes = 28672;  // decode buckets + cdf in LDS beside the 132 KiB ring (k_decode)
 constexpr uint64_t kMaxMinHead = 1ull << 56;
@@ -163,26 +165,34 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     // ring at offset 0 (64 KiB), rows after it
     double* rcps = reinterpret_cast<double*>(lds + kEncRingBytes);
     uint2* mcs = reinterpret_cast<uint2*>(lds + kEncRingBytes + kEncMcOffset);  // immediate ds offset from rcps
-    uint64_t* pks = reinterpret_cast<uint64_t*>(lds + kEncRingBytes + kEncPkOffset);
+    uint64_t* thrs = reinterpret_cast<uint64_t*>(lds + kEncRingBytes + kEncThrOffset);
     if (!kGlobalRows) {
         for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) {
             const EncRow r = t.enc[i];
             rcps[i] = r.rcp;
             mcs[i] = make_uint2(r.mass, r.cum);
-            pks[i] = static_cast<uint64_t>(r.mass) * t.K;  // renorm bound p*K (src/ans.rs:100)
+            // renorm bound p*K (src/ans.rs:100): (head >> 8j) >= p*K  <=>  head > p*K*2^(8j) - 1,
+            // saturated at 2^64 - 1 (never exceeded) when p*K*2^(8j) >= 2^64
+            const uint64_t pK = static_cast<uint64_t>(r.mass) * t.K;
+#pragma unroll
+            for (int j = 1; j <= KMAX; ++j)
+                thrs[(j - 1) * 257 + i] = (pK == 0 || (pK >> (64 - 8 * j)) != 0) ? ~0ull : (pK << (8 * j)) - 1;
         }
     }
-    // a row in registers: the table row plus its renorm bound p*K (read from LDS, or formed)
+    // a row in registers: the table row plus its KMAX renorm thresholds (from LDS)
     struct Row {
         EncRow e;
-        uint64_t pK;
+        uint64_t thr[KMAX];
     };
     auto row = [&](uint32_t s) __attribute__((always_inline)) {
         uint32_t off;  // 8*s + table base in one v_lshl_add (the base exceeds the ds offset field)
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(off) : "v"(s), "s"(kEncRingBytes));
         const uint64_t mc = lds_ld64(off + kEncMcOffset);
-        return Row{EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)},
-                   lds_ld64(off + kEncPkOffset)};
+        Row r;
+        r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) r.thr[j] = lds_ld64(off + kEncThrOffset + 8 * 257 * j);
+        return r;
     };
     const Ring ring{4 * threadIdx.x};
     __syncthreads();
@@ -216,13 +226,22 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto bound = [&](const EncRow& e) __attribute__((always_inline)) {
         return kK32 ? static_cast<uint64_t>(e.mass) * static_cast<uint32_t>(K) : static_cast<uint64_t>(e.mass) * K;
     };
-    auto push_one = [&](const EncRow& e, uint64_t pK) __attribute__((always_inline)) {
-        asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
-        // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
+    // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
+    auto bytes_out = [&](uint64_t pK) __attribute__((always_inline)) {
         uint32_t k = (head >> 8) >= pK ? 1u : 0u;
         if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 1u : 0u;
         if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 1u : 0u;
         if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
+        return k;
+    };
+    auto bytes_out_thr = [&](const uint64_t* thr) __attribute__((always_inline)) {  // the same, no shifts
+        uint32_t k = 0;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) k += head > thr[j] ? 1u : 0u;
+        return k;
+    };
+    auto push_one = [&](const EncRow& e, uint32_t k) __attribute__((always_inline)) {
+        asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
         f.push<KMAX>(lo32(head), k, ring);
         head >>= 8 * k;
         // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
@@ -244,7 +263,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             __builtin_amdgcn_sched_barrier(0);
             const Row e = e_next;
             if (j > 0) e_next = row(min(sym_of<Sym>(unit, j - 1), sentinel));
-            push_one(e.e, e.pK);
+            push_one(e.e, bytes_out_thr(e.thr));
         }
     };
     auto request_rows = [&](const uint4& unit, EncRow* buf) __attribute__((always_inline)) {
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     };
     auto process_rows = [&](const EncRow* buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = U - 1; j >= 0; --j) push_one(buf[j], bound(buf[j]));
+        for (int j = U - 1; j >= 0; --j) push_one(buf[j], bytes_out(bound(buf[j])));
     };
 
     // (non-temporal symbol loads / page stores measured 28% SLOWER with rows in global memory)
