@@ -459,7 +459,8 @@ struct DecChain {
         wy = lds_ld32(a);
         wx = lds_ld32(a + 4 * kDecBlock);
     }
-    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P) & 3u); }
+    // (v_alignbyte_b32 reads only the low two bits of its shift operand: P needs no mask)
+    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
     // the top two pages land before decoding starts; the third is requested
     __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
         src = s;
@@ -690,7 +691,7 @@ struct DecChainG {
         wy = a[0];
         wx = a[kBlock];
     }
-    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P) & 3u); }
+    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }  // low 2 bits used
     // the top four pages land before decoding starts; the next two are requested
     __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
         src = s;
