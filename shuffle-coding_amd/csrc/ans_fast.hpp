@@ -36,7 +36,7 @@ constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 constexpr uint32_t kEncMcOffset = 8 * 257;
 constexpr uint32_t kEncThrOffset = 2 * kEncMcOffset;
 constexpr uint32_t kEncLdsBytes = (6 * kEncMcOffset + 15) & ~15u;
-constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB at LDS offset 0
+constexpr uint32_t kEncRingBytes = (kRingDwords + 1) * kBlock * 4;  // 66 KiB at LDS offset 0 (+ mirror row)
 constexpr uint32_t kDecTableBytes = 28672;  // decode buckets + cdf in LDS beside the 132 KiB ring (k_decode)
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
@@ -111,27 +111,38 @@ __device__ __forceinline__ void put_sym(uint4& v, int j, uint32_t s) {
 }
 
 // ====================================================================== encode
-// Byte funnel: (a1:a0) holds n stream bytes MSB-aligned, oldest lowest (n <= 3 between pushes).
-// Pushing k bytes shifts the head's low k bytes in at the top; each completed 4 bytes are a
-// little-endian stream dword and go to the ring.
+// Byte funnel.  pos8 = 8 * (stream bytes so far), neg8 = -pos8; the stream's dword w = pos/4
+// lives in ring row w & 31 (row 32 mirrors row 0 for writes only), and X holds its contents
+// with the b = pos & 3 written bytes at the bottom (garbage above).  A push of the head's low k
+// bytes (lo, little-endian = stream order, src/ans.rs:246-253) writes both dwords it can touch
+// with one ds_write2st64_b32, whatever k is:
+//   dword w   = X's b bytes | lo << 8b           (v_bfe_u32 + v_lshl_or_b32)
+//   dword w+1 = lo >> (32 - 8b)                  (v_lshrrev_b32; for b = 0 all of lo: unused bytes)
+// Bytes past the new end are garbage that the next push overwrites (every push rewrites its whole
+// dword w).  Row 32 only ever receives a dword that has just been entered (b' < 4 bytes of it), so
+// the next push, which rewrites that dword in row 0, lands before the page holding it is read.
 struct Funnel {
-    uint32_t a0, a1, n, wd;  // wd = stream dwords completed
+    uint32_t X, pos8, neg8, addr, col;  // addr = ring address of dword pos/4 (row | col)
 
-    template <int KMAX>
-    __device__ __forceinline__ void push(uint32_t lo, uint32_t k, const Ring& ring) {
-        uint32_t b0 = ab(a1, a0, k), b1 = ab(lo, a1, k);
-        if constexpr (KMAX >= 4) {
-            b0 = k == 4 ? a1 : b0;
-            b1 = k == 4 ? lo : b1;
-        }
-        a0 = b0;
-        a1 = b1;
-        n += k;
-        // oldest 4 bytes; written unconditionally (a partial dword is rewritten once complete)
-        ring.at(static_cast<int32_t>(wd)) = n == 4 ? a1 : ab(a1, a0, 8 - n);
-        const uint32_t full = n >= 4 ? 1u : 0u;
-        wd += full;
-        n -= 4 * full;
+    __device__ __forceinline__ void push(uint32_t lo, uint32_t k8) {
+        uint32_t xv, d0, d1;
+        asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
+        asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d0) : "v"(lo), "v"(pos8), "v"(xv));
+        asm("v_lshrrev_b32 %0, %1, %2" : "=v"(d1) : "v"(neg8), "v"(lo));
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = d0;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + 2048u)) = d1;  // next row
+        pos8 += k8;
+        neg8 -= k8;
+        const uint32_t a = ((pos8 << 6) & 0xF800u) | col;
+        X = a != addr ? d1 : d0;
+        addr = a;
+    }
+    __device__ __forceinline__ uint32_t len() const { return pos8 >> 3; }
+    // the partial last dword, zero-padded, into its ring row (nothing is pushed after this)
+    __device__ __forceinline__ void finish() {
+        uint32_t xv;
+        asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = xv;
     }
 };
 
@@ -162,7 +173,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     extern __shared__ __align__(16) unsigned char lds[];
     // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
     // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
-    // ring at offset 0 (64 KiB), rows after it
+    // ring at offset 0 (66 KiB), rows after it
     double* rcps = reinterpret_cast<double*>(lds + kEncRingBytes);
     uint2* mcs = reinterpret_cast<uint2*>(lds + kEncRingBytes + kEncMcOffset);  // immediate ds offset from rcps
     uint64_t* thrs = reinterpret_cast<uint64_t*>(lds + kEncRingBytes + kEncThrOffset);
@@ -209,7 +220,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     const uint32_t sentinel = t.enc_rows - 1;  // zero-mass row: out-of-range symbols land here
 
     uint64_t head = kMaxMinHead;  // Message::zeros()
-    Funnel f{0, 0, 0, 0};
+    Funnel f{0, 0, 0, ring.col, ring.col};
     uint32_t fp = 0, over = 0;
     uint32_t minmass = ~0u;  // 0 after a zero-mass / out-of-range symbol; accumulated by an
                              // opaque v_min so the compiler cannot sink the test to the loop end
@@ -217,7 +228,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 
     auto point = [&]() __attribute__((always_inline)) {
         wait_vm();
-        if ((f.wd >> 4) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
+        if ((f.pos8 >> 9) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
             if (fp < npages_cap) flush_page(ring, fp, dst);
             else over = 1;
             ++fp;
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     };
     auto push_one = [&](const EncRow& e, uint32_t k) __attribute__((always_inline)) {
         asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
-        f.push<KMAX>(lo32(head), k, ring);
+        f.push(lo32(head), 8 * k);
         head >>= 8 * k;
         // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
         // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q' in {q, q+1} and
@@ -332,15 +343,15 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             process(c0);
         }
     }
-    wait_vm();
+    point();  // the last unit's completed page: the flatten's 8 bytes may reach the ring slot it holds
 
     // flatten (src/ans.rs:255-260): all significant head bytes, low first (7 or 8 here,
     // since the head is >= norm*K > 2^55 after any push).
     const uint32_t nb = (71u - static_cast<uint32_t>(__builtin_clzll(head))) >> 3;
-    f.push<4>(lo32(head), 4, ring);
-    f.push<4>(hi32(head), nb - 4, ring);
-    if (f.n) ring.at(static_cast<int32_t>(f.wd)) = f.a1 >> (8 * (4 - f.n));
-    const uint32_t len = 4 * f.wd + f.n;
+    f.push(lo32(head), 32);
+    f.push(hi32(head), 8 * (nb - 4));
+    f.finish();
+    const uint32_t len = f.len();
     for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
         if (fp < npages_cap) flush_page(ring, fp, dst);
         else over = 1;
