@@ -1,0 +1,88 @@
+"""Same-process A/B of two builds of the library on the C3 bench workload.
+
+usage: python tools/inproc_ab.py <libdir A> <libdir B> [iters]
+  libdir: a directory under shuffle-coding_amd/ holding libshufflecoding_amd.so ("lib" = default)
+
+Both builds are loaded side by side (RTLD_LOCAL, each registers its own code object) and run
+alternately on the same device-resident symbols, so clocks and the box are shared; the kernel
+times are HIP events on one explicit stream.  Prints the median encode / decode ms of each.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "shuffle-coding_amd"))
+import ans_amd as A  # noqa: E402
+import bench  # noqa: E402
+
+
+def load(d):
+    L = ctypes.CDLL(os.path.join(HERE, "..", "shuffle-coding_amd", d, "libshufflecoding_amd.so"))
+    for name, (res, args) in A.SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+def main():
+    dirs = sys.argv[1:3]
+    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+    masses_fn, log2n, sym_bytes, seed = bench.CONFIGS["c3"]
+    n, L = 1 << log2n, 4096
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    libs = [load(d) for d in dirs]
+    setups = []
+    syms = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for i, Lb in enumerate(libs):
+        A._lib = Lb
+        gpu = A.Gpu(0)
+        gt = A.GpuTable(gpu, A.Categorical(masses_fn()))
+        if i == 0:
+            gt.dev_gen_iid(seed, 0, n, syms, sym_bytes, stream)
+        cap = gt.slot_capacity(L)
+        nch = -(-n // L)
+        setups.append(dict(gpu=gpu, gt=gt, cap=cap,
+                           slots=torch.empty(nch * cap, dtype=torch.uint8, device="cuda"),
+                           lens=torch.zeros(nch, dtype=torch.int32, device="cuda"),
+                           status=torch.zeros(1, dtype=torch.int32, device="cuda"),
+                           out=torch.empty_like(syms)))
+
+    def step(i, ev):
+        A._lib = libs[i]
+        s = setups[i]
+        ev[0].record(stream)
+        s["gt"].dev_encode(syms, sym_bytes, n, L, s["slots"], s["cap"], s["lens"], s["status"], stream)
+        ev[1].record(stream)
+        s["gt"].dev_decode(s["slots"], None, s["cap"], s["lens"], n, L, s["out"], sym_bytes, s["status"], stream)
+        ev[2].record(stream)
+
+    for _ in range(3):
+        for i in range(2):
+            step(i, [torch.cuda.Event(enable_timing=True) for _ in range(3)])
+    torch.cuda.synchronize()
+    evs = [[], []]
+    for _ in range(iters):
+        for i in range(2):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            step(i, ev)
+            evs[i].append(ev)
+        torch.cuda.synchronize()
+    for i in range(2):
+        s = setups[i]
+        assert torch.equal(s["out"], syms), f"{dirs[i]}: round trip differs"
+        enc = np.median([e[0].elapsed_time(e[1]) for e in evs[i]])
+        dec = np.median([e[1].elapsed_time(e[2]) for e in evs[i]])
+        print(f"{dirs[i]:10s} enc {enc:.4f} dec {dec:.4f} ms (median of {iters})")
+    assert torch.equal(setups[0]["lens"], setups[1]["lens"]), "the two builds' stream lengths differ"
+
+
+if __name__ == "__main__":
+    main()
