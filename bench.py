@@ -47,8 +47,8 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)  # the clocks ramp over the first ~5 steps
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--log2n", type=int, default=None, help="symbols per rank = 2^log2n (default: the config's)")
     p.add_argument("--chunk-len", type=int, default=4096)

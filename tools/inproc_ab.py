@@ -33,6 +33,7 @@ def load(d):
 def main():
     dirs = sys.argv[1:3]
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+    sync = os.environ.get("AB_NOSYNC") != "1"  # AB_NOSYNC=1: back-to-back launches, no idle gaps
     masses_fn, log2n, sym_bytes, seed = bench.CONFIGS["c3"]
     n, L = 1 << log2n, 4096
     torch.cuda.set_device(0)
@@ -74,13 +75,17 @@ def main():
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             step(i, ev)
             evs[i].append(ev)
-        torch.cuda.synchronize()
+        if sync:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
     for i in range(2):
         s = setups[i]
         assert torch.equal(s["out"], syms), f"{dirs[i]}: round trip differs"
         enc = np.median([e[0].elapsed_time(e[1]) for e in evs[i]])
         dec = np.median([e[1].elapsed_time(e[2]) for e in evs[i]])
-        print(f"{dirs[i]:10s} enc {enc:.4f} dec {dec:.4f} ms (median of {iters})")
+        print(f"{dirs[i]:10s} enc {enc:.4f} dec {dec:.4f} ms (median of {iters}{'' if sync else ', no sync'})")
+        if os.environ.get("AB_TRACE") == "1":
+            print(" ".join(f"{e[0].elapsed_time(e[1]):.3f}/{e[1].elapsed_time(e[2]):.3f}" for e in evs[i]))
     assert torch.equal(setups[0]["lens"], setups[1]["lens"]), "the two builds' stream lengths differ"
 
 
