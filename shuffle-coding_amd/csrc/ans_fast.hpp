@@ -164,7 +164,11 @@ __device__ __forceinline__ void flush_page(const Ring& ring, uint32_t p, uint8_t
 // kGlobalRows: the rows stay in global memory (alphabets above 256 symbols, e.g. C4's 65,536:
 // 1 MiB of rows, L2-resident); each unit's rows are then requested at the point BEFORE the
 // unit that uses them, so their latency hides behind one unit of work.
-template <typename Sym, int KMAX, bool kK32, bool kGlobalRows>
+// kRare (LDS rows only): the rows whose threshold KMAX is below 2^64 are rare (C3: one symbol of
+// probability 1e-5).  Every row then reads KMAX - 1 thresholds; those rare rows carry a negative
+// rcp and add the last threshold's test on a wave-voted branch (one 8-byte LDS read, one
+// 64-bit compare and one add fewer per symbol).
+template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kRare = false>
 __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTable t, const Sym* __restrict__ syms,
                                                                          uint64_t chunk_len, uint64_t nfull,
                                                                          uint8_t* __restrict__ slots, uint64_t slot_cap,
@@ -180,20 +184,25 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     if (!kGlobalRows) {
         for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) {
             const EncRow r = t.enc[i];
-            rcps[i] = r.rcp;
             mcs[i] = make_uint2(r.mass, r.cum);
             // renorm bound p*K (src/ans.rs:100): (head >> 8j) >= p*K  <=>  head > p*K*2^(8j) - 1,
             // saturated at 2^64 - 1 (never exceeded) when p*K*2^(8j) >= 2^64
             const uint64_t pK = static_cast<uint64_t>(r.mass) * t.K;
+            uint64_t last = ~0ull;
 #pragma unroll
-            for (int j = 1; j <= KMAX; ++j)
-                thrs[(j - 1) * 257 + i] = (pK == 0 || (pK >> (64 - 8 * j)) != 0) ? ~0ull : (pK << (8 * j)) - 1;
+            for (int j = 1; j <= KMAX; ++j) {
+                last = (pK == 0 || (pK >> (64 - 8 * j)) != 0) ? ~0ull : (pK << (8 * j)) - 1;
+                thrs[(j - 1) * 257 + i] = last;
+            }
+            rcps[i] = (kRare && last != ~0ull) ? -r.rcp : r.rcp;  // the rare-row flag
         }
     }
-    // a row in registers: the table row plus its KMAX renorm thresholds (from LDS)
+    // a row in registers: the table row plus its first KF renorm thresholds (from LDS)
+    constexpr int KF = kRare ? KMAX - 1 : KMAX;
     struct Row {
         EncRow e;
-        uint64_t thr[KMAX];
+        uint64_t thr[KF];
+        uint32_t off;
     };
     auto row = [&](uint32_t s) __attribute__((always_inline)) {
         uint32_t off;  // 8*s + table base in one v_lshl_add (the base exceeds the ds offset field)
@@ -202,7 +211,8 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         Row r;
         r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) r.thr[j] = lds_ld64(off + kEncThrOffset + 8 * 257 * j);
+        for (int j = 0; j < KF; ++j) r.thr[j] = lds_ld64(off + kEncThrOffset + 8 * 257 * j);
+        r.off = off;
         return r;
     };
     const Ring ring{4 * threadIdx.x};
@@ -248,7 +258,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto bytes_out_thr = [&](const uint64_t* thr) __attribute__((always_inline)) {  // the same, no shifts
         uint32_t k = 0;
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) k += head > thr[j] ? 1u : 0u;
+        for (int j = 0; j < KF; ++j) k += head > thr[j] ? 1u : 0u;
         return k;
     };
     auto push_one = [&](const EncRow& e, uint32_t k) __attribute__((always_inline)) {
@@ -274,7 +284,20 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             __builtin_amdgcn_sched_barrier(0);
             const Row e = e_next;
             if (j > 0) e_next = row(min(sym_of<Sym>(unit, j - 1), sentinel));
-            push_one(e.e, bytes_out_thr(e.thr));
+            uint32_t k = bytes_out_thr(e.thr);
+            if constexpr (kRare) {
+                EncRow r = e.e;
+                const bool rare = static_cast<int32_t>(hi32(static_cast<uint64_t>(__double_as_longlong(r.rcp)))) < 0;
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
+                    if (rare) {
+                        k += head > lds_ld64(e.off + kEncThrOffset + 8 * 257 * (KMAX - 1)) ? 1u : 0u;
+                        r.rcp = -r.rcp;
+                    }
+                }
+                push_one(r, k);
+            } else {
+                push_one(e.e, k);
+            }
         }
     };
     auto request_rows = [&](const uint4& unit, EncRow* buf) __attribute__((always_inline)) {

@@ -458,22 +458,26 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         const size_t lds = ft.enc_lds_bytes + fast::kEncRingBytes;
         const bool k32 = ft.K < (1ull << 32);
-#define ENC(KM, K32, G) fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
-#define ENC_KMAX(G)                                                   \
-        switch (ft.kmax) {                                            \
-        case 1:                                                       \
-        case 2: if (k32) ENC(2, true, G); else ENC(2, false, G); break; \
-        case 3: if (k32) ENC(3, true, G); else ENC(3, false, G); break; \
-        default: if (k32) ENC(4, true, G); else ENC(4, false, G); break; \
+#define ENC(KM, K32, G, R) fast::k_encode<Sym, KM, K32, G, R><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
+#define ENC_KMAX(G, R)                                                         \
+        switch (ft.kmax) {                                                     \
+        case 1: if (k32) ENC(2, true, G, false); else ENC(2, false, G, false); break; \
+        case 2: if (k32) ENC(2, true, G, R); else ENC(2, false, G, R); break;  \
+        case 3: if (k32) ENC(3, true, G, R); else ENC(3, false, G, R); break;  \
+        default: if (k32) ENC(4, true, G, R); else ENC(4, false, G, R); break; \
         }
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_global) {
-                ENC_KMAX(true)
+                ENC_KMAX(true, false)
+            } else if (ft.enc_rare) {
+                ENC_KMAX(false, true)
             } else {
-                ENC_KMAX(false)
+                ENC_KMAX(false, false)
             }
+        } else if (ft.enc_rare) {
+            ENC_KMAX(false, true)
         } else {
-            ENC_KMAX(false)
+            ENC_KMAX(false, false)
         }
 #undef ENC_KMAX
 #undef ENC
@@ -649,6 +653,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const uint32_t nsym = t.nsym;
     std::vector<EncRow> enc(nsym + 1);
     uint32_t kmax = 1;
+    std::vector<uint32_t> kmax_row(nsym + 1, 0);
     for (uint32_t s = 0; s <= nsym; ++s) {
         const uint64_t m = s < nsym ? cat.masses[s] : 0;
         enc[s] = EncRow{m ? 1.0 / static_cast<double>(m) : 0.0, static_cast<uint32_t>(m),
@@ -656,8 +661,14 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         if (!m) continue;
         const u128 pK = static_cast<u128>(m) * t.K;
         for (uint32_t j = 1; j <= 4; ++j)  // can a push emit j bytes? (head < 2^64 <= p*K*2^8j otherwise)
-            if ((pK << (8 * j)) < (static_cast<u128>(1) << 64) && j > kmax) kmax = j;
+            if ((pK << (8 * j)) < (static_cast<u128>(1) << 64)) kmax_row[s] = j;
+        kmax = std::max(kmax, kmax_row[s]);
     }
+    // rows that reach kmax: rare enough (by mass) for a wave-voted slow path?
+    u128 rare_mass = 0;
+    for (uint32_t s = 0; s < nsym; ++s)
+        if (kmax_row[s] == kmax) rare_mass += cat.masses[s];
+    ft.enc_rare = kmax >= 2 && (rare_mass << 10) <= t.norm;
     ft.enc_global = nsym > 256;
     ft.dec_usable = nsym <= 256;
     // decode buckets: the finest power-of-two width whose table fits fast::kDecTableBytes in

@@ -90,6 +90,8 @@ struct FastTable {
     uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
     uint32_t dec_global;  // decode fast path for nsym > 256 (k_decode_g, buckets in global memory)
     uint32_t dec_far;     // some LDS bucket holds three or more cdf boundaries (slow path needed)
+    uint32_t enc_rare;    // the rows that can emit kmax bytes carry at most 2^-10 of the mass:
+                          // the encoder's fast path tests kmax - 1 thresholds (ans_fast.hpp kRare)
 };
 
 }  // namespace shuffle_coding

@@ -501,6 +501,28 @@ def test_boundary_tables_bit_exact(gpu, name):
     _roundtrip_vs_oracle(gpu, masses, syms, 4096, np.uint8 if len(masses) <= 256 else np.uint16)
 
 
+def test_rare_rows_whole_waves(gpu):
+    """The encoder's rare-row path (ans_fast.hpp kRare: rows that can emit kmax bytes hold at most
+    2^-10 of the mass, so they are tested on a wave-voted branch) under data made of them: chunks
+    of only rare symbols (every lane of a wave on the slow path), half rare, and one rare symbol
+    in an otherwise common chunk.  (CPU-checkable precondition: the table does select kRare.)"""
+    masses = _tables_at_the_boundaries()["kmax_4"]
+    norm, K = int(masses.sum()), (1 << 56) // int(masses.sum())
+    kmax_row = [max([j for j in range(1, 5) if (int(m) * K) << (8 * j) < 1 << 64], default=0) for m in masses]
+    kmax = max(kmax_row)
+    rare = [s for s, k in enumerate(kmax_row) if k == kmax]
+    assert kmax == 4 and sum(int(masses[s]) for s in rare) << 10 <= norm
+    rng = np.random.default_rng(41)
+    L, nch = 4096, 192
+    common = np.flatnonzero(np.asarray(kmax_row) < kmax)
+    syms = rng.choice(common, size=(nch, L))
+    syms[:64] = rng.choice(rare, size=(64, L))                      # waves of rare rows only
+    half = rng.random((64, L)) < 0.5
+    syms[64:128][half] = rng.choice(rare, size=int(half.sum()))
+    syms[128:, 1000] = rare[0]                                      # one lane-step each
+    _roundtrip_vs_oracle(gpu, masses, syms.reshape(-1).astype(np.uint32), L, np.uint8)
+
+
 # ---------------------------------------------------------------- variable-length chunks
 @pytest.mark.parametrize("which", ["c3", "multiset", "tiny_norm"])
 def test_var_chunks_bit_exact(gpu, which, multiset_masses):
