@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                 last = (pK == 0 || (pK >> (64 - 8 * j)) != 0) ? ~0ull : (pK << (8 * j)) - 1;
                 thrs[(j - 1) * 257 + i] = last;
             }
-            rcps[i] = (kRare && last != ~0ull) ? -r.rcp : r.rcp;  // the rare-row flag
+            rcps[i] = (kRare && (last != ~0ull || r.mass == 0)) ? -r.rcp : r.rcp;  // the rare-row flag
         }
     }
     // a row in registers: the table row plus its first KF renorm thresholds (from LDS)
@@ -255,16 +255,19 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
         return k;
     };
-    auto bytes_out_thr = [&](const uint64_t* thr) __attribute__((always_inline)) {  // the same, no shifts
-        uint32_t k = 0;
+    // the same as 8k, no shifts: the thresholds grow with j (saturated ones stay saturated), so
+    // the last one exceeded gives k, and the count is one v_cndmask per threshold
+    auto bytes_out_thr8 = [&](const uint64_t* thr) __attribute__((always_inline)) {
+        uint32_t k8 = 0;
 #pragma unroll
-        for (int j = 0; j < KF; ++j) k += head > thr[j] ? 1u : 0u;
-        return k;
+        for (int j = 0; j < KF; ++j) k8 = head > thr[j] ? 8u * (j + 1) : k8;
+        return k8;
     };
-    auto push_one = [&](const EncRow& e, uint32_t k) __attribute__((always_inline)) {
-        asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
-        f.push(lo32(head), 8 * k);
-        head >>= 8 * k;
+    // kRare kernels flag zero-mass rows as rare and take their mass on the voted branch
+    auto push_one = [&](const EncRow& e, uint32_t k8) __attribute__((always_inline)) {
+        if constexpr (!kRare) asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
+        f.push(lo32(head), k8);
+        head >>= k8;
         // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
         // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q' in {q, q+1} and
         // r' = head - q'*p in (-p, p): head = norm*q' + (cum + r' + [r' < 0]*(p - norm)),
@@ -284,19 +287,20 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             __builtin_amdgcn_sched_barrier(0);
             const Row e = e_next;
             if (j > 0) e_next = row(min(sym_of<Sym>(unit, j - 1), sentinel));
-            uint32_t k = bytes_out_thr(e.thr);
+            uint32_t k8 = bytes_out_thr8(e.thr);
             if constexpr (kRare) {
                 EncRow r = e.e;
                 const bool rare = static_cast<int32_t>(hi32(static_cast<uint64_t>(__double_as_longlong(r.rcp)))) < 0;
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
                     if (rare) {
-                        k += head > lds_ld64(e.off + kEncThrOffset + 8 * 257 * (KMAX - 1)) ? 1u : 0u;
+                        k8 = head > lds_ld64(e.off + kEncThrOffset + 8 * 257 * (KMAX - 1)) ? 8u * KMAX : k8;
+                        minmass = min(minmass, r.mass);
                         r.rcp = -r.rcp;
                     }
                 }
-                push_one(r, k);
+                push_one(r, k8);
             } else {
-                push_one(e.e, k);
+                push_one(e.e, k8);
             }
         }
     };
@@ -306,7 +310,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     };
     auto process_rows = [&](const EncRow* buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = U - 1; j >= 0; --j) push_one(buf[j], bytes_out(bound(buf[j])));
+        for (int j = U - 1; j >= 0; --j) push_one(buf[j], 8 * bytes_out(bound(buf[j])));
     };
 
     // (non-temporal symbol loads / page stores measured 28% SLOWER with rows in global memory)
