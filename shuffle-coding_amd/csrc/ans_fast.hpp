@@ -406,11 +406,14 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 // 64-bit test runs only when some lane of the wave passes the 32-bit screen (a uniform
 // branch; the common path is js bytes with no select).  hL8 = ~0 when L = 2^56 (hi32(L) << 8
 // would overflow, and X >> 8 < 2^56 = L never needs one byte less).
+// kJ4 = false: no pop leaves the high word zero (kmax <= 3: p*K >= 2^32 for every symbol, and
+// a pop leaves head >= p*q >= p*K), so js = clz >> 3 needs no clamp.
+template <bool kJ4 = true>
 __device__ __forceinline__ uint32_t renorm_up(uint64_t& head, uint32_t W, uint64_t L, uint32_t hL8) {
     const uint32_t h1 = hi32(head), h0 = lo32(head);
     uint32_t fb;
     asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
-    const uint32_t js = min(fb >> 3, 4u);
+    const uint32_t js = kJ4 ? min(fb >> 3, 4u) : fb >> 3;
     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(js, js, 0u);
     const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
     head = mk64(xj1, xj0);
@@ -532,9 +535,10 @@ struct DecChain {
         }
     }
     // phase 1: renorm_up, q/cf, next window
+    template <bool kJ4>
     __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
         form_window();
-        P -= static_cast<int32_t>(renorm_up(head, W, L, hL8));
+        P -= static_cast<int32_t>(renorm_up<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
@@ -585,8 +589,8 @@ struct DecChain {
 
 // SPP: symbols per point (U, or U/2 when U*KMAX > 60: u8 tables whose pops can take 4 bytes).
 // kFar: some bucket holds more than four cdf boundaries, so the voted slow path is compiled in.
-// kP24: every mass is below 2^24 (DecChain::update).
-template <typename Sym, int SPP, bool kFar, bool kP24>
+// kP24: every mass is below 2^24 (DecChain::update).  kJ4: some pop can pull 4 bytes (kmax = 4).
+template <typename Sym, int SPP, bool kFar, bool kP24, bool kJ4>
 __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
@@ -642,7 +646,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                 ch.point();
             }
             __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
-            ch.renorm_div(L, hL8, norm, rcp_norm);
+            ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
 #ifdef ANS_PAD_VALU  // experiment: independent filler VALU per symbol (issue- vs latency-bound)
 #pragma unroll
             for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));

@@ -522,13 +522,15 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
-#define DEC(SPP, FAR, P24) fast::k_decode<Sym, SPP, FAR, P24><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
-#define DEC_P(SPP, FAR) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true); else DEC(SPP, FAR, false)
-            if (U * ft.kmax > 60) {
-                if (ft.dec_far) { DEC_P(U / 2, true); } else { DEC_P(U / 2, false); }
+#define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
+#define DEC_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true, J4); else DEC(SPP, FAR, false, J4)
+#define DEC_J(SPP, FAR) if (ft.kmax >= 4) { DEC_P(SPP, FAR, true); } else { DEC_P(SPP, FAR, false); }
+            if (U * ft.kmax > 60) {  // (kmax = 4)
+                if (ft.dec_far) { DEC_P(U / 2, true, true); } else { DEC_P(U / 2, false, true); }
             } else {
-                if (ft.dec_far) { DEC_P(U, true); } else { DEC_P(U, false); }
+                if (ft.dec_far) { DEC_J(U, true); } else { DEC_J(U, false); }
             }
+#undef DEC_J
 #undef DEC_P
 #undef DEC
         }
