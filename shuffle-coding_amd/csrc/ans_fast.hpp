@@ -453,6 +453,7 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
 // so the whole 160 KiB of LDS holds the 1,024 rings (132 KiB) plus 28 KiB of tables, twice the
 // table room two 512-lane workgroups would leave (finer icdf buckets: C3 resolves every cf with
 // three candidates and compiles no far path).
+__device__ const uint4 kZeroPage[4] = {};  // 64 zero bytes: the Zeros tail generator's pages
 constexpr int kDecBlock = 1024;
 constexpr int kDecRows = 33;
 constexpr uint32_t kDecRingBytes = kDecRows * kDecBlock * 4;
@@ -482,14 +483,17 @@ struct DecChain {
         }
         if ((p & 1) == 0) row(32) = S[0].x;
     }
+    // pages below 0 come from a zero page in global memory: the same four loads, where a
+    // register zero-fill cost the point 16 v_mov on every wave with one lane at its stream start
+    // (global address space: a flat load would also count in lgkmcnt and stall the LDS waits)
     __device__ __forceinline__ void fetch_page(int32_t p) {
-        if (p >= 0) {
-            const uint4* g = reinterpret_cast<const uint4*>(src + 64ll * p);
+        typedef __attribute__((address_space(1))) const v4u32 gv4;
+        const uint4* g = p >= 0 ? reinterpret_cast<const uint4*>(src + 64ll * p) : kZeroPage;
+        const gv4* gg = reinterpret_cast<const gv4*>(reinterpret_cast<uintptr_t>(g));
 #pragma unroll
-            for (int k = 0; k < 4; ++k) S[k] = g[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) S[k] = make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < 4; ++k) {
+            const v4u32 v = gg[k];
+            S[k] = make_uint4(v.x, v.y, v.z, v.w);
         }
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
