@@ -12,7 +12,7 @@ rc=$?; echo "smoke rc=$rc: $(tail -1 $O/smoke.log)"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 $O/bench.log; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 PMC_META="--config c3 --log2n 30" bash tools/pmc.sh $TAG > $O/pmc.log 2>&1
 rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || { tail $O/pmc.log; exit $rc; }
