@@ -71,6 +71,17 @@ __device__ __forceinline__ uint64_t qest(uint64_t x, double rcp) {
     return static_cast<uint64_t>(__double_as_longlong(t)) - 0x4330000000000000ull;
 }
 
+// qest - 1 (floor - 1 or floor) from the magic constant 2^52 - 1, for x / d >= 1: the sum lands
+// at or above 2^52, where the ulp is 1, so it still rounds to an integer.
+__device__ __forceinline__ uint64_t qest_m1(uint64_t x, double rcp) {
+    double hd;
+    asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(x)));
+    const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(x)));
+    double t;  // v_fma_f64 (from C++ the compiler copies the magic into a v_fmac accumulator)
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "v"(xd), "v"(rcp), "v"(4503599627370495.0));
+    return static_cast<uint64_t>(__double_as_longlong(t));  // raw bits: qest - 1 + 0x43300000'00000000
+}
+
 // Lane-private ring of 32 dwords in a [dword][lane] image.
 // LDS accesses by byte offset (address space 3): keeps the address arithmetic in 32 bits
 // where the compiler otherwise adds the (zero) LDS base or splits constants out of offsets.
@@ -228,6 +239,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     const uint64_t norm = t.norm;
     const uint64_t K = t.K;
     const uint32_t sentinel = t.enc_rows - 1;  // zero-mass row: out-of-range symbols land here
+    const uint32_t exp_norm = 0x43300000u * static_cast<uint32_t>(t.norm);  // qest_m1's exponent word x norm
 
     uint64_t head = kMaxMinHead;  // Message::zeros()
     Funnel f{0, 0, 0, ring.col, ring.col};
@@ -269,14 +281,19 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         f.push(lo32(head), k8);
         head >>= k8;
         // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
-        // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q' in {q, q+1} and
-        // r' = head - q'*p in (-p, p): head = norm*q' + (cum + r' + [r' < 0]*(p - norm)),
-        // a signed 32-bit addend, so the q' - 1 fix-up never touches 64 bits.
-        const uint64_t q = qest(head, e.rcp);
-        const int32_t rr = static_cast<int32_t>(lo32(head) - lo32(q) * e.mass);
-        const int32_t adj = rr < 0 ? static_cast<int32_t>(e.mass - static_cast<uint32_t>(norm)) : 0;
-        const int32_t a = static_cast<int32_t>(e.cum) + rr + adj;
-        head = q * norm + static_cast<uint64_t>(static_cast<int64_t>(a));
+        // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q_m in {q - 1, q} (head >= p*K
+        // >= p after the renorm, so q >= 1) and r_m = head - q_m*p in [0, 2p):
+        // head = norm*q_m + (cum + r_m + [r_m >= p]*(norm - p)), an addend in [0, 2 norm), so
+        // the q_m + 1 fix-up never touches 64 bits and needs no sign extension.
+        const uint64_t qb = qest_m1(head, e.rcp);  // q_m = qb - 0x43300000'00000000
+        const uint32_t rm = lo32(head) - lo32(qb) * e.mass;
+        const uint32_t a = e.cum + rm + (rm >= e.mass ? static_cast<uint32_t>(norm) - e.mass : 0u);
+        // the high word as v_mul_lo_u32 + v_add3 on the raw exponent word (its 0x43300000 * norm
+        // comes off as a scalar): a second v_mad_u64_u32 costs two v_mov and the exponent a v_add
+        const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * static_cast<uint32_t>(norm) + a;
+        uint32_t hq;
+        asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb)), "s"(static_cast<uint32_t>(norm)));
+        head = mk64(hi32(lo64) + hq - exp_norm, lo32(lo64));
     };
     auto process = [&](const uint4& unit) __attribute__((always_inline)) {
         // rows are read one symbol ahead; the scheduling barriers keep the compiler from
