@@ -36,7 +36,13 @@ constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 constexpr uint32_t kEncMcOffset = 8 * 257;
 constexpr uint32_t kEncThrOffset = 2 * kEncMcOffset;
 constexpr uint32_t kEncLdsBytes = (6 * kEncMcOffset + 15) & ~15u;
-constexpr uint32_t kEncRingBytes = (kRingDwords + 1) * kBlock * 4;  // 66 KiB at LDS offset 0 (+ mirror row)
+constexpr uint32_t kEncRingBytes = (kRingDwords + 1) * kBlock * 4;  // 66 KiB (+ mirror row)
+// encode LDS: the row tables at offset 0 (a row address is the symbol times 8, each array at an
+// immediate offset), the ring after them at a multiple of 256 B (the ds_write2st64 offset unit),
+// so its row addresses stay one v_and_or with the ring base in the instructions' offset field
+constexpr uint32_t kEncRingBase = (kEncLdsBytes + 255) & ~255u;
+constexpr uint32_t kEncSharedBytes = kEncRingBase + kEncRingBytes;
+static_assert(2 * kEncSharedBytes <= 160 * 1024, "two encode workgroups per CU");
 constexpr uint32_t kDecTableBytes = 28672;  // decode buckets + cdf in LDS beside the 132 KiB ring (k_decode)
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
@@ -95,12 +101,12 @@ __device__ __forceinline__ uint4 lds_ld128(uint32_t off) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// (kept at LDS offset 0: a row address is one v_and_or of the row bits and the lane's column)
+// at kEncRingBase: a row address is one v_and_or of the row bits and the lane's column
 struct Ring {
     uint32_t col;  // 4 * lane
     __device__ __forceinline__ lds_u32& at(int32_t i) const {
         const uint32_t a = ((static_cast<uint32_t>(i) << 11) & 0xF800u) | col;
-        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a));
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a + kEncRingBase));
     }
 };
 
@@ -140,8 +146,8 @@ struct Funnel {
         asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
         asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d0) : "v"(lo), "v"(pos8), "v"(xv));
         asm("v_lshrrev_b32 %0, %1, %2" : "=v"(d1) : "v"(neg8), "v"(lo));
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = d0;
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + 2048u)) = d1;  // next row
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase)) = d0;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase + 2048u)) = d1;  // next row
         pos8 += k8;
         neg8 -= k8;
         const uint32_t a = ((pos8 << 6) & 0xF800u) | col;
@@ -153,7 +159,7 @@ struct Funnel {
     __device__ __forceinline__ void finish() {
         uint32_t xv;
         asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = xv;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase)) = xv;
     }
 };
 
@@ -188,13 +194,17 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     extern __shared__ __align__(16) unsigned char lds[];
     // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
     // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
-    // ring at offset 0 (66 KiB), rows after it
-    double* rcps = reinterpret_cast<double*>(lds + kEncRingBytes);
-    uint2* mcs = reinterpret_cast<uint2*>(lds + kEncRingBytes + kEncMcOffset);  // immediate ds offset from rcps
-    uint64_t* thrs = reinterpret_cast<uint64_t*>(lds + kEncRingBytes + kEncThrOffset);
+    // rows at offset 0, ring after them (kEncRingBase)
+    double* rcps = reinterpret_cast<double*>(lds);
+    uint2* mcs = reinterpret_cast<uint2*>(lds + kEncMcOffset);  // immediate ds offset from rcps
+    uint64_t* thrs = reinterpret_cast<uint64_t*>(lds + kEncThrOffset);
+    // u8 symbols index the rows unclamped: all 256 byte values get a row (zero mass beyond the
+    // alphabet, so they fail like the sentinel row they used to be clamped to)
+    constexpr bool kByteRows = sizeof(Sym) == 1;
     if (!kGlobalRows) {
-        for (uint32_t i = threadIdx.x; i < t.enc_rows; i += kBlock) {
-            const EncRow r = t.enc[i];
+        const uint32_t nrows = kByteRows ? 256u : t.enc_rows;
+        for (uint32_t i = threadIdx.x; i < nrows; i += kBlock) {
+            const EncRow r = i < t.enc_rows ? t.enc[i] : EncRow{0.0, 0u, 0u};
             mcs[i] = make_uint2(r.mass, r.cum);
             // renorm bound p*K (src/ans.rs:100): (head >> 8j) >= p*K  <=>  head > p*K*2^(8j) - 1,
             // saturated at 2^64 - 1 (never exceeded) when p*K*2^(8j) >= 2^64
@@ -216,8 +226,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         uint32_t off;
     };
     auto row = [&](uint32_t s) __attribute__((always_inline)) {
-        uint32_t off;  // 8*s + table base in one v_lshl_add (the base exceeds the ds offset field)
-        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(off) : "v"(s), "s"(kEncRingBytes));
+        const uint32_t off = 8 * s;  // the tables sit at LDS offset 0
         const uint64_t mc = lds_ld64(off + kEncMcOffset);
         Row r;
         r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
@@ -298,12 +307,15 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto process = [&](const uint4& unit) __attribute__((always_inline)) {
         // rows are read one symbol ahead; the scheduling barriers keep the compiler from
         // hoisting all sixteen reads (and their registers) to the top of the unit
-        Row e_next = row(min(sym_of<Sym>(unit, U - 1), sentinel));
+        auto rsym = [&](int j) __attribute__((always_inline)) {
+            return kByteRows ? sym_of<Sym>(unit, j) : min(sym_of<Sym>(unit, j), sentinel);
+        };
+        Row e_next = row(rsym(U - 1));
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             __builtin_amdgcn_sched_barrier(0);
             const Row e = e_next;
-            if (j > 0) e_next = row(min(sym_of<Sym>(unit, j - 1), sentinel));
+            if (j > 0) e_next = row(rsym(j - 1));
             uint32_t k8 = bytes_out_thr8(e.thr);
             if constexpr (kRare) {
                 EncRow r = e.e;

@@ -456,7 +456,7 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     if (nfull) {
         const FastTable& ft = gt->ft;
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
-        const size_t lds = ft.enc_lds_bytes + fast::kEncRingBytes;
+        const size_t lds = fast::kEncSharedBytes;  // rows (LDS-row kernels) + ring
         const bool k32 = ft.K < (1ull << 32);
 #define ENC(KM, K32, G, R) fast::k_encode<Sym, KM, K32, G, R><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
 #define ENC_KMAX(G, R)                                                         \
