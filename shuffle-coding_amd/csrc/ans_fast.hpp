@@ -44,6 +44,13 @@ constexpr uint32_t kEncRingBase = (kEncLdsBytes + 255) & ~255u;
 constexpr uint32_t kEncSharedBytes = kEncRingBase + kEncRingBytes;
 static_assert(2 * kEncSharedBytes <= 160 * 1024, "two encode workgroups per CU");
 constexpr uint32_t kDecTableBytes = 28672;  // decode buckets + cdf in LDS beside the 132 KiB ring (k_decode)
+// fixed decode table layout (LDS offset 0, and the same in global memory): kDecNbMax 16-B buckets,
+// their s0 bytes at kDecS0Off (a compile-time ds offset from the bucket index), the cdf table
+// (nsym + 5 <= 261 words) at kDecCumOff
+constexpr uint32_t kDecNbMax = (kDecTableBytes - 4 * 261 - 16) / 17;
+constexpr uint32_t kDecS0Off = 16 * kDecNbMax;
+constexpr uint32_t kDecCumOff = (kDecS0Off + kDecNbMax + 15) & ~15u;
+static_assert(kDecCumOff + 4 * 261 <= kDecTableBytes, "decode tables fit");
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // Non-temporal 16-byte global load / store (streamed data that must not evict cached tables).
@@ -93,6 +100,7 @@ __device__ __forceinline__ uint64_t qest_m1(uint64_t x, double rcp) {
 // where the compiler otherwise adds the (zero) LDS base or splits constants out of offsets.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t off) { return *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(off)); }
 __device__ __forceinline__ uint64_t lds_ld64(uint32_t off) { return *reinterpret_cast<const lds_u64*>(static_cast<uintptr_t>(off)); }
 typedef __attribute__((address_space(3))) v4u32 lds_v4u32;
@@ -472,7 +480,7 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
 // ====================================================================== decode
 // One decode chain = one chunk, read from the end.  P is the stream position minus 4: the
 // window W = stream bytes [P, P+4) (byte P+3 on top) comes from ring dwords y = P>>2 and y+1
-// with one v_alignbyte.  The ring (LDS offset 0; tables after it) is [row][lane] with kDecRows = 33 rows:
+// with one v_alignbyte.  The ring (after the tables, at kDecTableBytes) is [row][lane] with kDecRows = 33 rows:
 // row 32 mirrors row 0, so y and y+1 are one ds_read2st64_b32 even across the wrap.  Pages
 // (16 rows) land at points: page low+1 is free once dword y+1 lies in page low, and the page
 // below `low` is always in flight in registers (S); pages below 0 are zeros (the Zeros
@@ -487,6 +495,10 @@ constexpr int kDecBlock = 1024;
 constexpr int kDecRows = 33;
 constexpr uint32_t kDecRingBytes = kDecRows * kDecBlock * 4;
 static_assert(kDecRingBytes + kDecTableBytes == 160 * 1024, "decode LDS = one CU's 160 KiB");
+// decode LDS: the tables at offset 0 (bucket = cf bucket * 16, its s0 byte at the bucket index
+// plus an immediate offset), the ring after them at kDecTableBytes (a multiple of 256 B, folded
+// into the window read's ds_read2st64 offsets)
+static_assert(kDecTableBytes % 256 == 0 && kDecTableBytes / 256 + 16 <= 255, "ring base in the st64 offsets");
 
 struct DecChain {
     uint32_t* ring;  // &ring[0][lane]
@@ -526,12 +538,12 @@ struct DecChain {
         }
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
-    // ring at LDS offset 0 the row address is one v_and_or of (P << 10) and the lane's column.
-    uint32_t wx, wy, col;  // col = 4 * lane: the lane's byte column in the ring (LDS offset 0)
+    // ring base in the ds offsets the row address is one v_and_or of (P << 10) and the lane's column.
+    uint32_t wx, wy, col;  // col = 4 * lane: the lane's byte column in the ring
     __device__ __forceinline__ void read_window() {
         const uint32_t a = ((static_cast<uint32_t>(P) << 10) & 0x1F000u) | col;  // row (P>>2)&31
-        wy = lds_ld32(a);
-        wx = lds_ld32(a + 4 * kDecBlock);
+        wy = lds_ld32(a + kDecTableBytes);
+        wx = lds_ld32(a + kDecTableBytes + 4 * kDecBlock);
     }
     // (v_alignbyte_b32 reads only the low two bits of its shift operand: P needs no mask)
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
@@ -579,13 +591,10 @@ struct DecChain {
     // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket:
     // c0..c3 in one ds_read_b128 (two compares pick among three candidates; cf >= c3 is the
     // voted far case), s0 from the array after the buckets.
-    __device__ __forceinline__ void lookup(uint32_t shift, uint32_t s0_base) {
+    __device__ __forceinline__ void lookup(uint32_t shift) {
         const uint32_t bi = cf >> shift;
-        uint32_t off, soff;  // table bases exceed the ds offset field: one v_lshl_add each
-        asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(off) : "v"(bi), "s"(kDecRingBytes));
-        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(soff) : "v"(bi), "s"(s0_base));
-        const uint4 c = lds_ld128(off);
-        const uint32_t s0 = lds_ld32(soff);
+        const uint4 c = lds_ld128(bi << 4);  // buckets at LDS offset 0
+        const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0Off));
         // the read completes here: the compiler otherwise defers parts a select needs only on
         // some lanes into branches, adding dependent LDS round trips
         asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
@@ -629,7 +638,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
                                                       uint32_t* __restrict__ status) {
     extern __shared__ __align__(16) unsigned char lds[];
-    unsigned char* tab = lds + kDecRingBytes;  // ring at offset 0, tables after it
+    unsigned char* tab = lds;  // tables at offset 0, ring after them
     {
         uint4* b = reinterpret_cast<uint4*>(tab);  // buckets and s0 array: dec_cum_off bytes
         const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt);
@@ -650,14 +659,13 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
-    const uint32_t s0_base = kDecRingBytes + t.dec_s0_off;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
 #ifdef ANS_PAD_VALU
     uint32_t pad_acc = threadIdx.x;
 #endif
     DecChain ch;
-    ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
+    ch.ring = reinterpret_cast<uint32_t*>(lds + kDecTableBytes) + threadIdx.x;
     ch.col = 4 * threadIdx.x;
     ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
@@ -684,7 +692,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
 #pragma unroll
             for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));
 #endif
-            ch.lookup(shift, s0_base);
+            ch.lookup(shift);
             if (kFar && __builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
             ch.template update<kP24>();
             put_sym<Sym>(outv, j, ch.sx);

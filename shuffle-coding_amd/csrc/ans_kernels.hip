@@ -681,21 +681,20 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         const char* e = getenv("ANS_DECG_BUCKET_BITS");
         return e ? static_cast<uint32_t>(atoi(e)) : 16u;
     }();
-    const uint64_t max_buckets =
-        ft.dec_usable ? (fast::kDecTableBytes - cum_bytes - 16) / (sizeof(DecBucket) + sizeof(uint32_t)) : (1ull << g_bits);
+    const uint64_t max_buckets = ft.dec_usable ? fast::kDecNbMax : (1ull << g_bits);
     while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > max_buckets) ++shift;
     const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1);
     std::vector<uint32_t> cum(nsym + 6, t.norm);
     for (uint32_t s = 0; s < nsym; ++s) cum[s] = static_cast<uint32_t>(cat.cummasses[s]);
     std::vector<DecBucket> dec(ft.dec_usable ? nb : 0);
-    std::vector<uint32_t> dec_s0(ft.dec_usable ? nb : 0);
+    std::vector<uint8_t> dec_s0(ft.dec_usable ? nb : 0);  // nsym <= 256: one byte each
     std::vector<DecBucketG> decg(ft.dec_usable ? 0 : nb);
     for (uint32_t j = 0; j < nb; ++j) {
         const uint32_t s0 = static_cast<uint32_t>(cat.icdf(static_cast<uint64_t>(j) << shift).first);
         if (ft.dec_usable) {
             DecBucket& d = dec[j];
             for (int i = 0; i < 4; ++i) d.c[i] = cum[s0 + i];
-            dec_s0[j] = s0;
+            dec_s0[j] = static_cast<uint8_t>(s0);
             // every cf of the bucket below cdf(s0 + 3)?  (the last bucket ends at norm)
             const uint64_t end = std::min<uint64_t>(t.norm, (static_cast<uint64_t>(j) + 1) << shift);
             if (d.c[3] < end) ft.dec_far = 1;
@@ -713,8 +712,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_shift = shift;
     ft.norm = t.norm;
     ft.enc_lds_bytes = fast::kEncLdsBytes;  // nsym + 1 <= 257 rows, split (ans_fast.hpp)
-    ft.dec_s0_off = static_cast<uint32_t>(sizeof(DecBucket) * dec.size());
-    ft.dec_cum_off = static_cast<uint32_t>((ft.dec_s0_off + sizeof(uint32_t) * dec_s0.size() + 15) & ~size_t(15));
+    ft.dec_s0_off = fast::kDecS0Off;  // fixed layout (ans_fast.hpp)
+    ft.dec_cum_off = fast::kDecCumOff;
     ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;
     ft.pmax = 0;
@@ -732,10 +731,12 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(base + o_dec, dec.data(), sizeof(DecBucket) * dec.size(), hipMemcpyHostToDevice));
-    if (!dec_s0.empty())
-        HIP_TRY(hipMemcpy(base + o_dec + ft.dec_s0_off, dec_s0.data(), sizeof(uint32_t) * dec_s0.size(),
-                          hipMemcpyHostToDevice));
+    if (!dec.empty()) {  // buckets at 0, s0 bytes at kDecS0Off (staged into LDS as one block)
+        std::vector<uint8_t> img(ft.dec_cum_off, 0);
+        std::memcpy(img.data(), dec.data(), sizeof(DecBucket) * dec.size());
+        std::memcpy(img.data() + ft.dec_s0_off, dec_s0.data(), dec_s0.size());
+        HIP_TRY(hipMemcpy(base + o_dec, img.data(), img.size(), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMemcpy(base + o_cum, cum.data(), sizeof(uint32_t) * cum.size(), hipMemcpyHostToDevice));
     if (decg_b) HIP_TRY(hipMemcpy(base + o_decg, decg.data(), decg_b, hipMemcpyHostToDevice));
     ft.dbkt_g = reinterpret_cast<const DecBucketG*>(base + o_decg);
