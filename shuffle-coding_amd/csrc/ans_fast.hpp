@@ -31,11 +31,11 @@ namespace fast {
 constexpr int kBlock = 512;      // 8 waves; 2 workgroups (16 waves) per CU
 constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
-// encode LDS after the ring: rcp[257], (mass, cum)[257], then the renorm thresholds
-// thr_j[257] = p*K*2^(8j) - 1 (saturated), j = 1..KMAX (at most 4)
+// encode LDS rows: rcp[257], (mass, cum)[257] and the first renorm threshold
+// thr[257] = p*K*2^8 - 1 (saturated at 2^64 - 1); the others follow from it (k_encode)
 constexpr uint32_t kEncMcOffset = 8 * 257;
 constexpr uint32_t kEncThrOffset = 2 * kEncMcOffset;
-constexpr uint32_t kEncLdsBytes = (6 * kEncMcOffset + 15) & ~15u;
+constexpr uint32_t kEncLdsBytes = (3 * kEncMcOffset + 15) & ~15u;
 constexpr uint32_t kEncRingBytes = (kRingDwords + 1) * kBlock * 4;  // 66 KiB (+ mirror row)
 // encode LDS: the row tables at offset 0 (a row address is the symbol times 8, each array at an
 // immediate offset), the ring after them at a multiple of 256 B (the ds_write2st64 offset unit),
@@ -217,30 +217,25 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             // renorm bound p*K (src/ans.rs:100): (head >> 8j) >= p*K  <=>  head > p*K*2^(8j) - 1,
             // saturated at 2^64 - 1 (never exceeded) when p*K*2^(8j) >= 2^64
             const uint64_t pK = static_cast<uint64_t>(r.mass) * t.K;
-            uint64_t last = ~0ull;
-#pragma unroll
-            for (int j = 1; j <= KMAX; ++j) {
-                last = (pK == 0 || (pK >> (64 - 8 * j)) != 0) ? ~0ull : (pK << (8 * j)) - 1;
-                thrs[(j - 1) * 257 + i] = last;
-            }
-            rcps[i] = (kRare && (last != ~0ull || r.mass == 0)) ? -r.rcp : r.rcp;  // the rare-row flag
+            thrs[i] = (pK == 0 || (pK >> 56) != 0) ? ~0ull : (pK << 8) - 1;
+            const bool last_open = pK != 0 && (pK >> (64 - 8 * KMAX)) == 0;  // threshold KMAX < 2^64
+            rcps[i] = (kRare && (last_open || r.mass == 0)) ? -r.rcp : r.rcp;  // the rare-row flag
         }
     }
-    // a row in registers: the table row plus its first KF renorm thresholds (from LDS)
+    // a row in registers: the table row plus its first renorm threshold (from LDS).  The kernel
+    // tests KF thresholds on the common path, j = 1..KF: head > p*K*2^(8j) - 1 is
+    // (head >> 8(j-1)) > thr, exactly (also where p*K*2^(8j) saturates: then head >> 8(j-1) < p*K*2^8)
     constexpr int KF = kRare ? KMAX - 1 : KMAX;
     struct Row {
         EncRow e;
-        uint64_t thr[KF];
-        uint32_t off;
+        uint64_t thr;
     };
     auto row = [&](uint32_t s) __attribute__((always_inline)) {
         const uint32_t off = 8 * s;  // the tables sit at LDS offset 0
         const uint64_t mc = lds_ld64(off + kEncMcOffset);
         Row r;
         r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
-#pragma unroll
-        for (int j = 0; j < KF; ++j) r.thr[j] = lds_ld64(off + kEncThrOffset + 8 * 257 * j);
-        r.off = off;
+        r.thr = lds_ld64(off + kEncThrOffset);
         return r;
     };
     const Ring ring{4 * threadIdx.x};
@@ -284,12 +279,13 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
         return k;
     };
-    // the same as 8k, no shifts: the thresholds grow with j (saturated ones stay saturated), so
-    // the last one exceeded gives k, and the count is one v_cndmask per threshold
-    auto bytes_out_thr8 = [&](const uint64_t* thr) __attribute__((always_inline)) {
+    // the same as 8k: the thresholds grow with j, so the last one exceeded gives k, and the
+    // count is one v_cndmask per threshold (one LDS row read instead of KF: the encoder is
+    // co-limited by LDS bandwidth and bank conflicts, and a 64-bit shift is cheaper)
+    auto bytes_out_thr8 = [&](uint64_t thr) __attribute__((always_inline)) {
         uint32_t k8 = 0;
 #pragma unroll
-        for (int j = 0; j < KF; ++j) k8 = head > thr[j] ? 8u * (j + 1) : k8;
+        for (int j = 0; j < KF; ++j) k8 = (head >> (8 * j)) > thr ? 8u * (j + 1) : k8;
         return k8;
     };
     // kRare kernels flag zero-mass rows as rare and take their mass on the voted branch
@@ -330,7 +326,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                 const bool rare = static_cast<int32_t>(hi32(static_cast<uint64_t>(__double_as_longlong(r.rcp)))) < 0;
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
                     if (rare) {
-                        k8 = head > lds_ld64(e.off + kEncThrOffset + 8 * 257 * (KMAX - 1)) ? 8u * KMAX : k8;
+                        k8 = (head >> (8 * (KMAX - 1))) > e.thr ? 8u * KMAX : k8;
                         minmass = min(minmass, r.mass);
                         r.rcp = -r.rcp;
                     }
