@@ -36,7 +36,7 @@ constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 constexpr uint32_t kEncMcOffset = 8 * 257;
 constexpr uint32_t kEncThrOffset = 2 * kEncMcOffset;
 constexpr uint32_t kEncLdsBytes = (3 * kEncMcOffset + 15) & ~15u;
-constexpr uint32_t kEncRingBytes = (kRingDwords + 1) * kBlock * 4;  // 66 KiB (+ mirror row)
+constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB
 // encode LDS: the row tables at offset 0 (a row address is the symbol times 8, each array at an
 // immediate offset), the ring after them at a multiple of 256 B (the ds_write2st64 offset unit),
 // so its row addresses stay one v_and_or with the ring base in the instructions' offset field
@@ -137,15 +137,14 @@ __device__ __forceinline__ void put_sym(uint4& v, int j, uint32_t s) {
 
 // ====================================================================== encode
 // Byte funnel.  pos8 = 8 * (stream bytes so far), neg8 = -pos8; the stream's dword w = pos/4
-// lives in ring row w & 31 (row 32 mirrors row 0 for writes only), and X holds its contents
-// with the b = pos & 3 written bytes at the bottom (garbage above).  A push of the head's low k
-// bytes (lo, little-endian = stream order, src/ans.rs:246-253) writes both dwords it can touch
-// with one ds_write2st64_b32, whatever k is:
+// lives in ring row w & 31, and X holds its contents with the b = pos & 3 written bytes at the
+// bottom (garbage above).  A push of the head's low k bytes (lo, little-endian = stream order,
+// src/ans.rs:246-253) forms both dwords it can touch, whatever k is:
 //   dword w   = X's b bytes | lo << 8b           (v_bfe_u32 + v_lshl_or_b32)
 //   dword w+1 = lo >> (32 - 8b)                  (v_lshrrev_b32; for b = 0 all of lo: unused bytes)
-// Bytes past the new end are garbage that the next push overwrites (every push rewrites its whole
-// dword w).  Row 32 only ever receives a dword that has just been entered (b' < 4 bytes of it), so
-// the next push, which rewrites that dword in row 0, lands before the page holding it is read.
+// and stores only dword w (one ds_write_b32).  Dword w+1, when the push reached it, becomes X:
+// the next push (or finish) stores it with its own bytes, before any page holding it completes.
+// Bytes past the new end are garbage that the next push overwrites.
 struct Funnel {
     uint32_t X, pos8, neg8, addr, col;  // addr = ring address of dword pos/4 (row | col)
 
@@ -155,7 +154,6 @@ struct Funnel {
         asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d0) : "v"(lo), "v"(pos8), "v"(xv));
         asm("v_lshrrev_b32 %0, %1, %2" : "=v"(d1) : "v"(neg8), "v"(lo));
         *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase)) = d0;
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase + 2048u)) = d1;  // next row
         pos8 += k8;
         neg8 -= k8;
         const uint32_t a = ((pos8 << 6) & 0xF800u) | col;
