@@ -44,7 +44,8 @@ constexpr uint32_t kEncRingBase = (kEncLdsBytes + 255) & ~255u;
 constexpr uint32_t kEncSharedBytes = kEncRingBase + kEncRingBytes;
 static_assert(2 * kEncSharedBytes <= 160 * 1024, "two encode workgroups per CU");
 constexpr uint32_t kDecTableBytes = 28672;  // decode buckets + cdf in LDS beside the 132 KiB ring (k_decode)
-// fixed decode table layout (LDS offset 0, and the same in global memory): kDecNbMax 16-B buckets,
+// fixed decode table layout (LDS offset 0, and the same in global memory): kDecNbMax buckets as
+// two arrays of 8-B halves (cdf(s0), cdf(s0+1) | cdf(s0+2), cdf(s0+3)),
 // their s0 bytes at kDecS0Off (a compile-time ds offset from the bucket index), the cdf table
 // (nsym + 5 <= 261 words) at kDecCumOff
 constexpr uint32_t kDecNbMax = (kDecTableBytes - 4 * 261 - 16) / 17;
@@ -587,7 +588,10 @@ struct DecChain {
     // voted far case), s0 from the array after the buckets.
     __device__ __forceinline__ void lookup(uint32_t shift) {
         const uint32_t bi = cf >> shift;
-        const uint4 c = lds_ld128(bi << 4);  // buckets at LDS offset 0
+        // the bucket as two 8-B halves from two arrays (c0,c1 | c2,c3): random 16-B rows cost
+        // more LDS bank-conflict cycles than two random 8-B reads
+        const uint64_t ca = lds_ld64(bi << 3), cb = lds_ld64((bi << 3) + 8 * kDecNbMax);
+        const uint4 c = make_uint4(lo32(ca), hi32(ca), lo32(cb), hi32(cb));
         const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0Off));
         // the read completes here: the compiler otherwise defers parts a select needs only on
         // some lanes into branches, adding dependent LDS round trips

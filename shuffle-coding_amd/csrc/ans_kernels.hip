@@ -733,7 +733,10 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
     if (!dec.empty()) {  // buckets at 0, s0 bytes at kDecS0Off (staged into LDS as one block)
         std::vector<uint8_t> img(ft.dec_cum_off, 0);
-        std::memcpy(img.data(), dec.data(), sizeof(DecBucket) * dec.size());
+        for (size_t j = 0; j < dec.size(); ++j) {  // halves (c0,c1) at 8j, (c2,c3) at 8 (kDecNbMax + j)
+            std::memcpy(img.data() + 8 * j, &dec[j].c[0], 8);
+            std::memcpy(img.data() + 8 * (fast::kDecNbMax + j), &dec[j].c[2], 8);
+        }
         std::memcpy(img.data() + ft.dec_s0_off, dec_s0.data(), dec_s0.size());
         HIP_TRY(hipMemcpy(base + o_dec, img.data(), img.size(), hipMemcpyHostToDevice));
     }
