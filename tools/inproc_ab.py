@@ -80,13 +80,15 @@ def main():
     torch.cuda.synchronize()
     for i in range(2):
         s = setups[i]
-        assert torch.equal(s["out"], syms), f"{dirs[i]}: round trip differs"
+        if os.environ.get("AB_NOCHECK") != "1":
+            assert torch.equal(s["out"], syms), f"{dirs[i]}: round trip differs"
         enc = np.median([e[0].elapsed_time(e[1]) for e in evs[i]])
         dec = np.median([e[1].elapsed_time(e[2]) for e in evs[i]])
         print(f"{dirs[i]:10s} enc {enc:.4f} dec {dec:.4f} ms (median of {iters}{'' if sync else ', no sync'})")
         if os.environ.get("AB_TRACE") == "1":
             print(" ".join(f"{e[0].elapsed_time(e[1]):.3f}/{e[1].elapsed_time(e[2]):.3f}" for e in evs[i]))
-    assert torch.equal(setups[0]["lens"], setups[1]["lens"]), "the two builds' stream lengths differ"
+    if os.environ.get("AB_NOCHECK") != "1":
+        assert torch.equal(setups[0]["lens"], setups[1]["lens"]), "the two builds' stream lengths differ"
 
 
 if __name__ == "__main__":
