@@ -828,7 +828,11 @@ struct DecChainG {
         div_norm(head, norm, rcp_norm, qq, cf);
     }
     __device__ __forceinline__ void lookup(const DecBucketG* __restrict__ bkt, uint32_t shift) {
+#ifdef ANS_HYP_GL1  // timing experiment only (wrong symbols): every bucket load hits a 2-KiB, L1-resident slice
+        const uint4* e = reinterpret_cast<const uint4*>(bkt + ((cf >> shift) & 63u));
+#else
         const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
+#endif
         uint4 a = e[0], b = e[1];  // c0..c3 | c4, c5, s0, -
         // both loads complete here (no loads sunk into the selects' branches)
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z));
@@ -836,7 +840,11 @@ struct DecChainG {
         cum = b4 ? b.x : (b3 ? a.w : (b2 ? a.z : (b1 ? a.y : a.x)));
         nxt = b4 ? b.y : (b3 ? b.x : (b2 ? a.w : (b1 ? a.z : a.y)));
         sx = b.z + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
+#ifdef ANS_HYP_GL1
+        far = false;
+#else
         far = cf >= b.y;
+#endif
     }
     __device__ __forceinline__ void lookup_far(const uint32_t* __restrict__ gcum) {
         if (far) {

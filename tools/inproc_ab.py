@@ -1,6 +1,7 @@
 """Same-process A/B of two builds of the library on the C3 bench workload.
 
 usage: python tools/inproc_ab.py <libdir A> <libdir B> [iters]
+  AB_CONFIG=c4 AB_LOG2N=29: another bench config / size (default: C3 at its full size)
   libdir: a directory under shuffle-coding_amd/ holding libshufflecoding_amd.so ("lib" = default)
 
 Both builds are loaded side by side (RTLD_LOCAL, each registers its own code object) and run
@@ -34,14 +35,15 @@ def main():
     dirs = sys.argv[1:3]
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     sync = os.environ.get("AB_NOSYNC") != "1"  # AB_NOSYNC=1: back-to-back launches, no idle gaps
-    masses_fn, log2n, sym_bytes, seed = bench.CONFIGS["c3"]
+    masses_fn, log2n, sym_bytes, seed = bench.CONFIGS[os.environ.get("AB_CONFIG", "c3")]
+    log2n = int(os.environ.get("AB_LOG2N", log2n))
     n, L = 1 << log2n, 4096
     torch.cuda.set_device(0)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     libs = [load(d) for d in dirs]
     setups = []
-    syms = torch.empty(n, dtype=torch.uint8, device="cuda")
+    syms = torch.empty(n, dtype={1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes], device="cuda")
     for i, Lb in enumerate(libs):
         A._lib = Lb
         gpu = A.Gpu(0)
