@@ -64,10 +64,10 @@ def lib_hash():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(kernel_key, config, log2n, chunk_len):
-    """HBM bytes per launch of `kernel_key` from a committed rocprofv3 PMC summary of the
-    same workload (profiles/*pmc*.json, written by tools/pmc_summary.py --json), preferring
-    one taken on this exact library build; (bytes, source file) or (None, None)."""
+def pmc_record(kernel_key, config, log2n, chunk_len):
+    """The rocprofv3 PMC record of `kernel_key` on the same workload from a committed summary
+    (profiles/*pmc*.json, written by tools/pmc_summary.py --json), preferring one taken on this
+    exact library build, then the latest round; (record, source file) or (None, None)."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -80,7 +80,7 @@ def pmc_traffic(kernel_key, config, log2n, chunk_len):
             continue
         rank = (d.get("lib_hash") == lib_hash(), path)
         if best is None or rank > best[0]:
-            best = (rank, k.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT))
+            best = (rank, k, os.path.relpath(path, ROOT))
     return (None, None) if best is None else (best[1], best[2])
 
 
@@ -205,7 +205,11 @@ def main():
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
     t = torch.tensor([elapsed, bad], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+    per_rank = [elapsed]
     if world > 1:
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        per_rank = [float(x[0].item()) for x in parts]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if t[1].item() > 0:
         msg = A.lib().ans_status_string(st).decode() if st else "decoded symbols differ"
@@ -217,8 +221,26 @@ def main():
 
     alg_bytes = n * sym_bytes + comp_bytes  # per launch, encode and decode alike
     dom_name, dom_ms = ("decode", dec_ms) if dec_ms >= enc_ms else ("encode", enc_ms)
+    dom_kernel = f"k_{dom_name}" + ("_g" if dom_name == "decode" and gt.decode_kernel(sym_bytes) == "global" else "")
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(f"k_{dom_name}", args.config, log2n, L)
+    rec, rec_src = pmc_record(dom_kernel, args.config, log2n, L)
+    traffic = None if rec is None else rec.get("hbm_bytes_per_launch")
+    valu = None
+    if rec is not None and "valu_per_wave" in rec.get("derived", {}):
+        # one wave = 64 lanes = 64 chunks, one VALU wave-instruction per lane-step;
+        # issue capacity: 4 SIMDs per CU, one wave64 VALU instruction per 4 cycles each (the
+        # 4-cycle class of tools/microbench.hip; simple 32-bit adds/logic issue in 2)
+        d = rec["derived"]
+        per_sym = d["valu_per_wave"] / L
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+        wave_instr = d["valu_per_wave"] * nchunks / 64
+        clk = d.get("clock_ghz")
+        valu = {
+            "instr_per_symbol": round(per_sym, 2),
+            "frac_at_2.4GHz": round(wave_instr * 4 / (cus * 4 * 2.4e9 * dom_ms * 1e-3), 4),
+            "clock_ghz_pmc": None if clk is None else round(clk, 3),
+            "frac_at_pmc_clock": None if clk is None else round(wave_instr * 4 / (cus * 4 * clk * 1e9 * d["duration_ns"] * 1e-9), 4),
+        }
 
     if rank == 0:
         line = {
@@ -243,6 +265,8 @@ def main():
                 "chunks_per_gpu": nchunks,
                 "parallelism": f"chunk-sharded x{world}, no collective",
             },
+            "per_rank_ms_per_step": {"min": round(1e3 * min(per_rank) / args.steps, 4),
+                                     "max": round(1e3 * max(per_rank) / args.steps, 4)},
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
             "encode_gib_s": round(n * sym_bytes / (enc_ms * 1e-3) / 2**30, 3),
@@ -251,13 +275,15 @@ def main():
             "parity": "round trip verified on device; byte parity: tests/test_gpu_parity.py",
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"k_{dom_name}",
+                "kernel": dom_kernel,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else round(traffic),
-                "traffic_src": traffic_src,
+                "traffic_over_alg": None if traffic is None else round(traffic / alg_bytes, 3),
+                "traffic_src": rec_src,
+                "valu": valu,
             },
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -129,6 +129,13 @@ int ans_gpu_set_batch_bytes(ans_gpu *g, uint64_t batch_bytes);
 /* uploads the table (and its derived reciprocal / icdf-bucket data) to the device */
 int ans_gpu_table_create(ans_gpu *g, const ans_table *t, ans_gpu_table **out);
 void ans_gpu_table_free(ans_gpu_table *gt);
+/* Which kernels full chunks of this table take (bit flags; chunks outside them, e.g. a ragged
+ * last chunk, take the generic one-lane-per-chunk kernels): */
+#define ANS_PATH_ENC_LDS 1u     /* fast encoder, rows staged in LDS (<= 256 symbols) */
+#define ANS_PATH_ENC_GLOBAL 2u  /* fast encoder, rows read from global memory (larger alphabets) */
+#define ANS_PATH_DEC_LDS 4u     /* fast decoder, icdf buckets in LDS */
+#define ANS_PATH_DEC_GLOBAL 8u  /* fast decoder, icdf buckets in global memory */
+int ans_gpu_table_paths(const ans_gpu_table *gt, uint32_t *paths);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);
 

@@ -26,6 +26,7 @@ LIB_PATH = os.environ.get("SHUFFLE_CODING_AMD_LIB") or os.path.join(HERE, "lib",
 ANS_OK, ANS_E_ZERO_MASS, ANS_E_EXHAUSTED, ANS_E_LEN, ANS_E_SYMBOL = 0, 1, 2, 3, 4
 ANS_E_NORM_RANGE, ANS_E_DEVICE, ANS_E_ALLOC, ANS_E_ARG, ANS_E_MISMATCH = 5, 6, 7, 8, 9
 GEN_ZEROS, GEN_EMPTY, GEN_RANDOM = 0, 1, 2
+ANS_PATH_ENC_LDS, ANS_PATH_ENC_GLOBAL, ANS_PATH_DEC_LDS, ANS_PATH_DEC_GLOBAL = 1, 2, 4, 8
 MAX_MIN_HEAD = 1 << 56
 MAX_SIZE = MAX_MIN_HEAD >> 10
 
@@ -74,6 +75,7 @@ SIGNATURES = {
     "ans_gpu_table_create": (ci, [vp, vp, ctypes.POINTER(vp)]),
     "ans_gpu_table_free": (None, [vp]),
     "ans_gpu_slot_capacity": (ci, [vp, u64, u64p]),
+    "ans_gpu_table_paths": (ci, [vp, ctypes.POINTER(ctypes.c_uint32)]),
     "ans_gpu_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_decode_chunks": (ci, [vp, vp, u64, vp, vp, u64, u64, ci, vp, ci]),
     "ans_dev_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, vp]),
@@ -619,6 +621,21 @@ class GpuTable:
         if h and _lib is not None:
             _lib.ans_gpu_table_free(h)
             self.h = None
+
+    def paths(self):
+        """ANS_PATH_* flags: which fast kernels full chunks of this table take."""
+        f = ctypes.c_uint32(0)
+        _check(lib().ans_gpu_table_paths(self.h, ctypes.byref(f)), "ans_gpu_table_paths")
+        return f.value
+
+    def decode_kernel(self, sym_bytes):
+        """'lds' (fast::k_decode), 'global' (fast::k_decode_g) or 'generic' for full chunks."""
+        p = self.paths()
+        if p & ANS_PATH_DEC_LDS:
+            return "lds"
+        if p & ANS_PATH_DEC_GLOBAL and sym_bytes > 1:
+            return "global"
+        return "generic"
 
     def slot_capacity(self, chunk_len):
         c = u64(0)

@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         atomicOr(status, 1u << (sym_err ? ANS_E_SYMBOL : ANS_E_ZERO_MASS));
     }
     if (over) atomicOr(status, 1u << ANS_E_LEN);
-    lens[c] = len;
+    lens[c] = (over || minmass == 0) ? 0u : len;  // no length past the slot reaches k_compact or a decoder
 }
 
 // ---- shared decode steps
@@ -659,9 +659,11 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t shift = t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
-#ifdef ANS_PAD_VALU
-    uint32_t pad_acc = threadIdx.x;
-#endif
+    // a stream longer than its slot is foreign or corrupt: its pages would lie past the slot
+    if (lens[c] > slot_cap) {
+        atomicOr(status, 1u << ANS_E_LEN);
+        return;
+    }
     DecChain ch;
     ch.ring = reinterpret_cast<uint32_t*>(lds + kDecTableBytes) + threadIdx.x;
     ch.col = 4 * threadIdx.x;
@@ -686,10 +688,6 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
             }
             __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
             ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
-#ifdef ANS_PAD_VALU  // experiment: independent filler VALU per symbol (issue- vs latency-bound)
-#pragma unroll
-            for (int z = 0; z < ANS_PAD_VALU; ++z) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_acc) : "v"(z));
-#endif
             ch.lookup(shift);
             if (kFar && __builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
             ch.template update<kP24>();
@@ -715,9 +713,6 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const int32_t remaining = ch.P + 4;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
-#ifdef ANS_PAD_VALU
-    if (pad_acc == 0xDEADBEEFu) atomicOr(status, 1u << 31);
-#endif
 }
 
 // ====================================================================== decode, large alphabets
@@ -828,11 +823,7 @@ struct DecChainG {
         div_norm(head, norm, rcp_norm, qq, cf);
     }
     __device__ __forceinline__ void lookup(const DecBucketG* __restrict__ bkt, uint32_t shift) {
-#ifdef ANS_HYP_GL1  // timing experiment only (wrong symbols): every bucket load hits a 2-KiB, L1-resident slice
-        const uint4* e = reinterpret_cast<const uint4*>(bkt + ((cf >> shift) & 63u));
-#else
         const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
-#endif
         uint4 a = e[0], b = e[1];  // c0..c3 | c4, c5, s0, -
         // both loads complete here (no loads sunk into the selects' branches)
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z));
@@ -840,11 +831,7 @@ struct DecChainG {
         cum = b4 ? b.x : (b3 ? a.w : (b2 ? a.z : (b1 ? a.y : a.x)));
         nxt = b4 ? b.y : (b3 ? b.x : (b2 ? a.w : (b1 ? a.z : a.y)));
         sx = b.z + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
-#ifdef ANS_HYP_GL1
-        far = false;
-#else
         far = cf >= b.y;
-#endif
     }
     __device__ __forceinline__ void lookup_far(const uint32_t* __restrict__ gcum) {
         if (far) {
@@ -876,6 +863,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
     const uint32_t shift = t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
+    if (lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
+        atomicOr(status, 1u << ANS_E_LEN);
+        return;
+    }
     DecChainG ch;
     ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
     ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));

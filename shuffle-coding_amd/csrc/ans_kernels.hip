@@ -183,7 +183,11 @@ __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __rest
     }
     sink.put(static_cast<uint32_t>(head) & 0xffu);
     const uint64_t len = sink.finish();
-    if (sink.overflow) raise_status(status, ANS_E_LEN);
+    if (sink.overflow) {  // no length past the slot reaches k_compact or a decoder
+        raise_status(status, ANS_E_LEN);
+        lens[c] = 0;
+        return;
+    }
     lens[c] = static_cast<uint32_t>(len);
 }
 
@@ -208,6 +212,8 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
     if (c >= nchunks) return;
     const uint64_t a = starts ? starts[c] : c * chunk_len;
     const uint64_t b = starts ? starts[c + 1] : min(a + chunk_len, n);
+    // slot layout: a stream longer than its slot is foreign or corrupt (it would read past it)
+    if (!offsets && lens[c] > slot_cap) { raise_status(status, ANS_E_LEN); return; }
     ByteSource src;
     src.init(in + (offsets ? offsets[c] : c * slot_cap), lens[c]);
     uint64_t head = 0;  // Message::unflatten
@@ -216,8 +222,11 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
     const uint32_t norm = t.norm;
     for (uint64_t k = a; k < b; ++k) {
         // renorm(norm * K) (src/ans.rs:109): renorm_up pulls tail bytes; renorm_down cannot
-        // fire (after a pop head < p*256K <= 256*L).
-        while (head < L) {
+        // fire (after a pop head < p*256K <= 256*L).  A valid stream needs at most 8 pulls
+        // (head >= 1 after any pop); more means zero bytes past an exhausted or corrupt
+        // stream, where the loop would never end.
+        for (int pulls = 0; head < L; ++pulls) {
+            if (pulls == 8) { raise_status(status, ANS_E_MISMATCH); return; }
             uint32_t byte = 0;
             if (src.pos) byte = src.pop();
             else {
@@ -243,7 +252,8 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
         out[k] = static_cast<Sym>(s);
     }
     // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310).
-    while (head < kMaxMinHead) {
+    for (int pulls = 0; head < kMaxMinHead; ++pulls) {
+        if (pulls == 8) { raise_status(status, ANS_E_MISMATCH); return; }
         uint32_t byte = 0;
         if (src.pos) byte = src.pop();
         else ++generated;
@@ -412,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ 
     if (c >= nchunks) return;
     const uint8_t* s = slots + c * slot_cap;
     uint8_t* d = out + offsets[c];
-    wave_copy(d, s, lens[c], lane);
+    wave_copy(d, s, static_cast<uint32_t>(min<uint64_t>(lens[c], slot_cap)), lane);  // never past the slot
 }
 
 // One wave per chunk copies a dense-container stream into its slot (the inverse of k_compact).
@@ -677,11 +687,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     // LDS (with the cdf table); for large alphabets, at most 2^16 buckets in global memory
     uint32_t shift = 0;
     const size_t cum_bytes = sizeof(uint32_t) * (nsym + 5);
-    static const uint32_t g_bits = [] {  // experiment knob: global bucket table size
-        const char* e = getenv("ANS_DECG_BUCKET_BITS");
-        return e ? static_cast<uint32_t>(atoi(e)) : 16u;
-    }();
-    const uint64_t max_buckets = ft.dec_usable ? fast::kDecNbMax : (1ull << g_bits);
+    const uint64_t max_buckets = ft.dec_usable ? fast::kDecNbMax : (1ull << 16);
     while (((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1 > max_buckets) ++shift;
     const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> shift) + 1);
     std::vector<uint32_t> cum(nsym + 6, t.norm);
@@ -1145,7 +1151,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_at(const uint8_t* __restrict
     const uint64_t sh = (out_addr + offs[nchunks + 1]) & 15;
     const uint8_t* s = slots + c * slot_cap;
     uint8_t* d = dense + sh + offs[c];
-    wave_copy(d, s, lens[c], lane);
+    wave_copy(d, s, static_cast<uint32_t>(min<uint64_t>(lens[c], slot_cap)), lane);
 }
 
 // Copy-out of one encoded batch to out + base (size and base from the scan); a batch that
@@ -1500,6 +1506,17 @@ void ans_gpu_table_free(ans_gpu_table* gt) {
     (void)hipFree(gt->d_mem);
     if (gt->d_fast) (void)hipFree(gt->d_fast);
     delete gt;
+}
+
+int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
+    if (!gt || !paths) return ANS_E_ARG;
+    const FastTable& ft = gt->ft;
+    uint32_t p = 0;
+    if (ft.usable) p |= ft.enc_global ? ANS_PATH_ENC_GLOBAL : ANS_PATH_ENC_LDS;
+    if (ft.usable && ft.dec_usable) p |= ANS_PATH_DEC_LDS;
+    if (ft.usable && ft.dec_global) p |= ANS_PATH_DEC_GLOBAL;
+    *paths = p;
+    return ANS_OK;
 }
 
 int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t* slot_cap) {

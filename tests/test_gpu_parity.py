@@ -143,6 +143,39 @@ def test_device_errors_mirror_reference_panics(gpu):
     assert e.value.code == A.ANS_E_NORM_RANGE
 
 
+@pytest.mark.parametrize("which", ["generic", "fast"])
+def test_corrupt_containers_end_with_an_error(gpu, which):
+    """Streams that are empty or all zero bytes under Message::zeros() never reach the head
+    interval: decode must end with ANS_E_MISMATCH (the reference's assert_eq!(initial, m),
+    src/ans.rs:56), not pull zeros forever; under Message::empty() it is ANS_E_EXHAUSTED
+    (src/ans.rs:144).  A slot-layout length past its slot is refused with ANS_E_LEN."""
+    torch = pytest.importorskip("torch")
+    if which == "generic":  # norm < 2^16 and a ragged chunk: the generic kernels
+        masses, n, chunk_len, sym_bytes = [5, 9, 1, 300, 17], 10, 4, 1
+    else:  # C3 table, full chunks: the fast kernels
+        masses, n, chunk_len, sym_bytes = A.c3_masses(), 4 * 4096, 4096, 1
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    nchunks = -(-n // chunk_len)
+    for nbytes in (0, 8, 40):
+        data = np.zeros(max(1, nchunks * nbytes), np.uint8)
+        offsets = np.arange(nchunks, dtype=np.uint64) * nbytes
+        lens = np.full(nchunks, nbytes, np.uint64)
+        with pytest.raises(A.AnsError) as e:
+            gt.decode_chunks(data, offsets, lens, n, chunk_len, np.uint8)
+        assert e.value.code == A.ANS_E_MISMATCH, nbytes
+        with pytest.raises(A.AnsError) as e:
+            gt.decode_chunks(data, offsets, lens, n, chunk_len, np.uint8, gen_kind=A.GEN_EMPTY)
+        assert e.value.code in (A.ANS_E_EXHAUSTED, A.ANS_E_MISMATCH), nbytes
+    stream = torch.cuda.Stream()
+    cap = gt.slot_capacity(chunk_len)
+    slots = torch.zeros(nchunks * cap, dtype=torch.uint8, device="cuda")
+    lens_d = torch.full((nchunks,), cap + 64, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gt.dev_decode(slots, None, cap, lens_d, n, chunk_len, out, sym_bytes, status, stream)
+    assert gpu.status(status, stream) == A.ANS_E_LEN
+
+
 def test_fast_kernel_errors(gpu):
     masses = A.c3_masses().copy()
     masses[7] = 0
@@ -178,7 +211,32 @@ def test_gen_iid_matches_oracle(gpu):
 
 
 # ---------------------------------------------------------------- full-size configs (device-resident)
-def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed, sample_chunks):
+def _oracle_slices(masses, seed, n, chunk_len, nslices=64):
+    """The oracle's streams of the whole workload, chunk-parallel on the host cores: contiguous
+    chunk ranges (slices), each generated and encoded on its own thread (ctypes releases the
+    GIL).  Returns [(c0, c1)], the lens of every chunk, and per slice the sha256 of its dense
+    bytes."""
+    from concurrent.futures import ThreadPoolExecutor
+    import os
+    nchunks = -(-n // chunk_len)
+    per = -(-nchunks // nslices)
+    bounds = [(c0, min(nchunks, c0 + per)) for c0 in range(0, nchunks, per)]
+
+    def work(b):
+        a, e = b[0] * chunk_len, min(n, b[1] * chunk_len)
+        syms = orc.gen_iid(masses, seed, a, e - a)
+        d, _, ln = orc.encode_chunks(masses, syms, chunk_len)
+        return ln, hashlib.sha256(d.tobytes()).hexdigest()
+
+    with ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1))) as ex:  # a GPU box's CPU share is 16
+        res = list(ex.map(work, bounds))
+    return bounds, np.concatenate([r[0] for r in res]).astype(np.int64), [r[1] for r in res]
+
+
+def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed):
+    """Device-resident encode + decode of the whole workload; EVERY chunk's length and the
+    bytes of the whole compacted stream (sha256 per slice of chunks) must equal the oracle's
+    (src/ans.rs:255-260), and decode must be lossless."""
     torch = pytest.importorskip("torch")
     dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
     gt = A.GpuTable(gpu, A.Categorical(masses))
@@ -196,34 +254,42 @@ def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed, sample_chunks)
     gt.dev_decode(slots, None, cap, lens, n, chunk_len, out, sym_bytes, status, stream)
     assert gpu.status(status, stream) == 0
     assert torch.equal(out, syms), "lossless round trip"
+    del out
+    # the dense container (the wire format) of every chunk
+    l64 = lens.to(torch.int64)
+    offs = torch.cumsum(l64, 0) - l64
+    total = int(l64.sum().item())
+    dense = torch.empty(total, dtype=torch.uint8, device="cuda")
+    gpu.compact(slots, cap, lens, offs, nchunks, dense, stream)
     torch.cuda.synchronize()
     torch.cuda.set_stream(torch.cuda.default_stream())
-    # bit-exact on a sample of chunks against the oracle
-    rng = np.random.default_rng(seed)
-    picks = sorted(set(rng.integers(0, nchunks, size=sample_chunks).tolist()) | {0, nchunks - 1})
-    lens_h = lens.cpu().numpy().astype(np.int64)
-    for j in picks:
-        a, b = j * chunk_len, min(n, (j + 1) * chunk_len)
-        ref_syms = orc.gen_iid(masses, seed, a, b - a)
-        got_syms = syms[a:b].cpu().numpy().astype(np.int64) & ((1 << (8 * sym_bytes)) - 1)
-        assert np.array_equal(got_syms, ref_syms)
-        od, _, ol = orc.encode_chunks(masses, ref_syms, chunk_len)
-        assert int(ol[0]) == lens_h[j]
-        got = slots[j * cap: j * cap + int(lens_h[j])].cpu().numpy()
-        assert got.tobytes() == od.tobytes(), f"chunk {j}"
-    return int(lens_h.sum())
+    lens_h = l64.cpu().numpy()
+    offs_h = offs.cpu().numpy()
+    dense_h = dense.cpu().numpy()
+    del slots, dense
+    # the device generator is the oracle's (spot check; the streams below depend on all of it)
+    ref = orc.gen_iid(masses, seed, n - 4096, 4096)
+    assert np.array_equal(syms[n - 4096:].cpu().numpy().astype(np.int64) & ((1 << (8 * sym_bytes)) - 1), ref)
+    bounds, olens, ohash = _oracle_slices(masses, seed, n, chunk_len)
+    assert np.array_equal(lens_h, olens), "every chunk's stream length"
+    for (c0, c1), h in zip(bounds, ohash):
+        a = int(offs_h[c0])
+        e = int(offs_h[c1]) if c1 < nchunks else total
+        assert hashlib.sha256(dense_h[a:e].tobytes()).hexdigest() == h, f"chunks [{c0}, {c1})"
+    return total
 
 
 def test_c3_one_gib_u8_round_trip(gpu):
-    # 2^30 u8 symbols, 256-symbol table (norm 139,224,331), chunk 4096
-    total = _device_roundtrip(gpu, A.c3_masses(), 1 << 30, 4096, 1, 1, 48)
+    # 2^30 u8 symbols, 256-symbol table (norm 139,224,331), chunk 4096;
+    # all 262,144 chunks byte-compared against the oracle
+    total = _device_roundtrip(gpu, A.c3_masses(), 1 << 30, 4096, 1, 1)
     bps = total / (1 << 30)
     assert 0.95 < bps < 0.99  # H = 7.738 bits -> ~0.967 B/symbol plus per-chunk flush
 
 
 def test_c4_shard_u16_round_trip(gpu):
-    # SURVEY.md §8d C4 table (65,536 symbols, norm 134,561,356); one 2^27-symbol shard
-    total = _device_roundtrip(gpu, A.c4_masses(), 1 << 27, 4096, 2, 2, 32)
+    # SURVEY.md §8d C4 table (65,536 symbols, norm 134,561,356); one 2^27-symbol shard, all chunks
+    total = _device_roundtrip(gpu, A.c4_masses(), 1 << 27, 4096, 2, 2)
     assert 1.9 < total / (1 << 27) < 2.1
 
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 
 #define ITERS 2048
 
@@ -87,8 +88,103 @@ KERNEL(k_cmp_u64_cnd, DECL64; unsigned a0 = threadIdx.x, INIT64,
        CMP64(b0, b1); CMP64(b1, b2); CMP64(b2, b3); CMP64(b3, b4); CMP64(b4, b5); CMP64(b5, b6); CMP64(b6, b7); CMP64(b7, b0),
        SINK64 + a0)
 
-int main() {
-    const int blocks = 256 * 8, threads = 256;
+
+#define OP3(INS)                                                                        \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a0) : "v"(a1), "v"(a2));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a1) : "v"(a2), "v"(a3));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a2) : "v"(a3), "v"(a4));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a3) : "v"(a4), "v"(a5));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a4) : "v"(a5), "v"(a6));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a5) : "v"(a6), "v"(a7));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a6) : "v"(a7), "v"(a0));                   \
+    asm volatile(INS " %0, %0, %1, %2" : "+v"(a7) : "v"(a0), "v"(a1))
+#define OP1(INS)                                                                        \
+    asm volatile(INS " %0, %1" : "=v"(a0) : "v"(a1));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a1) : "v"(a2));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a2) : "v"(a3));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a3) : "v"(a4));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a4) : "v"(a5));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a5) : "v"(a6));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a6) : "v"(a7));                                    \
+    asm volatile(INS " %0, %1" : "=v"(a7) : "v"(a0))
+#define CMP32(D, S) asm volatile("v_cmp_ge_u32 vcc, %0, %1\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(D) : "v"(S) : "vcc")
+#define OPCMP32 CMP32(a0, a1); CMP32(a1, a2); CMP32(a2, a3); CMP32(a3, a4); CMP32(a4, a5); CMP32(a5, a6); CMP32(a6, a7); CMP32(a7, a0)
+#define MULF(D, S) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(D) : "v"(S))
+#define OPMULF MULF(d0, d1); MULF(d1, d2); MULF(d2, d3); MULF(d3, d4); MULF(d4, d5); MULF(d5, d6); MULF(d6, d7); MULF(d7, d0)
+#define ADDF(D, S) asm volatile("v_add_f64 %0, %0, %1" : "+v"(D) : "v"(S))
+#define OPADDF ADDF(d0, d1); ADDF(d1, d2); ADDF(d2, d3); ADDF(d3, d4); ADDF(d4, d5); ADDF(d5, d6); ADDF(d6, d7); ADDF(d7, d0)
+typedef float f2v __attribute__((ext_vector_type(2)));
+#define DECLP f2v p0, p1, p2, p3, p4, p5, p6, p7
+#define INITP p0 = f2v{(float)threadIdx.x, 1.f}; p1 = p0 + 1; p2 = p0 + 2; p3 = p0 + 3; p4 = p0 + 4; p5 = p0 + 5; p6 = p0 + 6; p7 = p0 + 7
+#define SINKP out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(p0 + p1 + p2 + p3 + p4 + p5 + p6 + p7).x
+#define PK(D, S) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(D) : "v"(S))
+#define OPPK PK(p0, p1); PK(p1, p2); PK(p2, p3); PK(p3, p4); PK(p4, p5); PK(p5, p6); PK(p6, p7); PK(p7, p0)
+
+KERNEL(k_alignbyte, DECL32, INIT32, OP3("v_alignbyte_b32"), SINK32)
+KERNEL(k_perm_b32, DECL32, INIT32, OP3("v_perm_b32"), SINK32)
+KERNEL(k_add3_u32, DECL32, INIT32, OP3("v_add3_u32"), SINK32)
+KERNEL(k_lshl_or_b32, DECL32, INIT32, OP3("v_lshl_or_b32"), SINK32)
+KERNEL(k_bfe_u32, DECL32, INIT32, OP3("v_bfe_u32"), SINK32)
+KERNEL(k_mad_u32_u24, DECL32, INIT32, OP3("v_mad_u32_u24"), SINK32)
+KERNEL(k_ffbh_u32, DECL32, INIT32, OP1("v_ffbh_u32"), SINK32)
+KERNEL(k_cvt_f32_u32, DECL32, INIT32, OP1("v_cvt_f32_u32"), SINK32)
+KERNEL(k_cvt_u32_f32, DECL32, INIT32, OP1("v_cvt_u32_f32"), SINK32)
+KERNEL(k_rcp_f32, DECL32, INIT32, OP1("v_rcp_f32"), SINK32)
+KERNEL(k_mul_f32, DECL32, INIT32, OP32("v_mul_f32"), SINK32)
+KERNEL(k_min_u32, DECL32, INIT32, OP32("v_min_u32"), SINK32)
+KERNEL(k_lshrrev_b32, DECL32, INIT32, OP32("v_lshrrev_b32"), SINK32)
+KERNEL(k_cmp_u32_cnd, DECL32, INIT32, OPCMP32, SINK32)
+KERNEL(k_mul_f64, DECLF, INITF, OPMULF, SINKF)
+KERNEL(k_add_f64, DECLF, INITF, OPADDF, SINKF)
+KERNEL(k_pk_fma_f32, DECLP, INITP, OPPK, SINKP)
+
+#define CND(D, S) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(D) : "v"(S))
+#define OPCND asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a0), "v"(a1) : "vcc"); CND(a0, a1); CND(a1, a2); CND(a2, a3); CND(a3, a4); CND(a4, a5); CND(a5, a6); CND(a6, a7); CND(a7, a0)
+#define CND64(D, S) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[10:11]" : "+v"(D) : "v"(S))
+#define OPCND64 asm volatile("v_cmp_gt_u32_e64 s[10:11], %0, %1" :: "v"(a0), "v"(a1) : "s10", "s11"); CND64(a0, a1); CND64(a1, a2); CND64(a2, a3); CND64(a3, a4); CND64(a4, a5); CND64(a5, a6); CND64(a6, a7); CND64(a7, a0)
+#define CMPO(D, S) asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(D), "v"(S) : "vcc")
+#define OPCMPONLY CMPO(a0, a1); CMPO(a1, a2); CMPO(a2, a3); CMPO(a3, a4); CMPO(a4, a5); CMPO(a5, a6); CMPO(a6, a7); CMPO(a7, a0); asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a0) : "v"(a1))
+#define ADDCO(D, S) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(D) : "v"(S) : "vcc")
+#define OPADDCO ADDCO(a0, a1); ADDCO(a1, a2); ADDCO(a2, a3); ADDCO(a3, a4); ADDCO(a4, a5); ADDCO(a5, a6); ADDCO(a6, a7); ADDCO(a7, a0)
+#define ADDC(D, S) asm volatile("v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(D) : "v"(S) : "vcc")
+#define OPADDC ADDC(a0, a1); ADDC(a1, a2); ADDC(a2, a3); ADDC(a3, a4); ADDC(a4, a5); ADDC(a5, a6); ADDC(a6, a7); ADDC(a7, a0)
+#define FMADEP(D) asm volatile("v_fma_f32 %0, %0, %0, %0" : "+v"(D))
+#define OPFMA32DEP FMADEP(f0); FMADEP(f0); FMADEP(f0); FMADEP(f0); FMADEP(f0); FMADEP(f0); FMADEP(f0); FMADEP(f0)
+#define ADDDEP(D) asm volatile("v_add_u32 %0, %0, %0" : "+v"(D))
+#define OPADDDEP ADDDEP(a0); ADDDEP(a0); ADDDEP(a0); ADDDEP(a0); ADDDEP(a0); ADDDEP(a0); ADDDEP(a0); ADDDEP(a0)
+#define MADDEP(D) asm volatile("v_mad_u64_u32 %0, vcc, %1, %1, %0" : "+v"(D) : "v"((unsigned)D) : "vcc")
+#define OPMADDEP MADDEP(b0); MADDEP(b0); MADDEP(b0); MADDEP(b0); MADDEP(b0); MADDEP(b0); MADDEP(b0); MADDEP(b0)
+#define FMAFDEP(D) asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(D))
+#define OPFMAFDEP FMAFDEP(d0); FMAFDEP(d0); FMAFDEP(d0); FMAFDEP(d0); FMAFDEP(d0); FMAFDEP(d0); FMAFDEP(d0); FMAFDEP(d0)
+#define PERMDEP(D) asm volatile("v_perm_b32 %0, %0, %0, %0" : "+v"(D))
+#define OPPERMDEP PERMDEP(a0); PERMDEP(a0); PERMDEP(a0); PERMDEP(a0); PERMDEP(a0); PERMDEP(a0); PERMDEP(a0); PERMDEP(a0)
+
+KERNEL(k_sub_u32, DECL32, INIT32, OP32("v_sub_u32"), SINK32)
+KERNEL(k_and_b32, DECL32, INIT32, OP32("v_and_b32"), SINK32)
+KERNEL(k_or_b32, DECL32, INIT32, OP32("v_or_b32"), SINK32)
+KERNEL(k_lshlrev_b32, DECL32, INIT32, OP32("v_lshlrev_b32"), SINK32)
+KERNEL(k_ashrrev_i32, DECL32, INIT32, OP32("v_ashrrev_i32"), SINK32)
+KERNEL(k_max_u32, DECL32, INIT32, OP32("v_max_u32"), SINK32)
+KERNEL(k_add_f32, DECL32, INIT32, OP32("v_add_f32"), SINK32)
+KERNEL(k_cndmask_e32, DECL32, INIT32, OPCND, SINK32)
+KERNEL(k_cndmask_e64, DECL32, INIT32, OPCND64, SINK32)
+KERNEL(k_cmp_e32, DECL32, INIT32, OPCMPONLY, SINK32)
+KERNEL(k_add_co, DECL32, INIT32, OPADDCO, SINK32)
+KERNEL(k_addc_co, DECL32, INIT32, OPADDC, SINK32)
+KERNEL(k_sub_f32_e64, DECL32, INIT32, OP32("v_sub_f32_e64"), SINK32)
+KERNEL(k_add_u32_e64, DECL32, INIT32, OP32("v_add_u32_e64"), SINK32)
+KERNEL(k_and_or_b32, DECL32, INIT32, OP3("v_and_or_b32"), SINK32)
+KERNEL(k_or3_b32, DECL32, INIT32, OP3("v_or3_b32"), SINK32)
+KERNEL(k_bfi_b32, DECL32, INIT32, OP3("v_bfi_b32"), SINK32)
+KERNEL(k_lshl_add_u32, DECL32, INIT32, OP3("v_lshl_add_u32"), SINK32)
+KERNEL(k_fma_f32_dep, DECLS, INITS, OPFMA32DEP, SINKS)
+KERNEL(k_add_u32_dep, DECL32, INIT32, OPADDDEP, SINK32)
+KERNEL(k_mad64_dep, DECL64, INIT64, OPMADDEP, SINK64)
+KERNEL(k_fma_f64_dep, DECLF, INITF, OPFMAFDEP, SINKF)
+KERNEL(k_perm_dep, DECL32, INIT32, OPPERMDEP, SINK32)
+
+int main(int argc, char** argv) {
+    const int blocks = 256 * (argc > 1 ? atoi(argv[1]) : 8), threads = 256;
     unsigned* out;
     hipMalloc(&out, sizeof(unsigned) * blocks * threads);
     hipEvent_t e0, e1;
@@ -106,6 +202,20 @@ int main() {
         {"v_lshl_add_u64", k_lshl_add_u64, 1}, {"v_fma_f64", k_fma_f64, 1},
         {"v_cvt_f64_u32", k_cvt_f64_u32, 1}, {"v_fma_f32", k_fma_f32, 1},
         {"v_cmp_ge_u64+v_cndmask", k_cmp_u64_cnd, 2},
+        {"v_alignbyte_b32", k_alignbyte, 1}, {"v_perm_b32", k_perm_b32, 1}, {"v_add3_u32", k_add3_u32, 1},
+        {"v_lshl_or_b32", k_lshl_or_b32, 1}, {"v_bfe_u32", k_bfe_u32, 1}, {"v_mad_u32_u24", k_mad_u32_u24, 1},
+        {"v_ffbh_u32", k_ffbh_u32, 1}, {"v_cvt_f32_u32", k_cvt_f32_u32, 1}, {"v_cvt_u32_f32", k_cvt_u32_f32, 1},
+        {"v_rcp_f32", k_rcp_f32, 1}, {"v_mul_f32", k_mul_f32, 1}, {"v_min_u32", k_min_u32, 1},
+        {"v_lshrrev_b32", k_lshrrev_b32, 1}, {"v_cmp_ge_u32+v_cndmask", k_cmp_u32_cnd, 2},
+        {"v_mul_f64", k_mul_f64, 1}, {"v_add_f64", k_add_f64, 1}, {"v_pk_fma_f32", k_pk_fma_f32, 1},
+        {"v_sub_u32", k_sub_u32, 1}, {"v_and_b32", k_and_b32, 1}, {"v_or_b32", k_or_b32, 1},
+        {"v_lshlrev_b32", k_lshlrev_b32, 1}, {"v_ashrrev_i32", k_ashrrev_i32, 1}, {"v_max_u32", k_max_u32, 1},
+        {"v_add_f32", k_add_f32, 1}, {"v_cndmask_e32", k_cndmask_e32, 1}, {"v_cndmask_e64", k_cndmask_e64, 1},
+        {"v_cmp_gt_u32_e32", k_cmp_e32, 1}, {"v_add_co_u32", k_add_co, 1}, {"v_addc_co_u32", k_addc_co, 1},
+        {"v_sub_f32_e64", k_sub_f32_e64, 1}, {"v_add_u32_e64", k_add_u32_e64, 1}, {"v_and_or_b32", k_and_or_b32, 1},
+        {"v_or3_b32", k_or3_b32, 1}, {"v_bfi_b32", k_bfi_b32, 1}, {"v_lshl_add_u32", k_lshl_add_u32, 1},
+        {"DEP v_fma_f32", k_fma_f32_dep, 1}, {"DEP v_add_u32", k_add_u32_dep, 1}, {"DEP v_mad_u64_u32", k_mad64_dep, 1},
+        {"DEP v_fma_f64", k_fma_f64_dep, 1}, {"DEP v_perm_b32", k_perm_dep, 1},
     };
     printf("clock(max) %.0f MHz, CUs %d\n", clk_hz / 1e6, prop.multiProcessorCount);
     for (auto& k : ks) {
