@@ -221,7 +221,9 @@ def main():
 
     alg_bytes = n * sym_bytes + comp_bytes  # per launch, encode and decode alike
     dom_name, dom_ms = ("decode", dec_ms) if dec_ms >= enc_ms else ("encode", enc_ms)
-    dom_kernel = f"k_{dom_name}" + ("_g" if dom_name == "decode" and gt.decode_kernel(sym_bytes) == "global" else "")
+    suffix = {"global": "_g", "wide": "_w"}.get(gt.decode_kernel(sym_bytes), "") if dom_name == "decode" else \
+        ("_w" if gt.paths() & A.ANS_PATH_ENC_WIDE else "")
+    dom_kernel = f"k_{dom_name}{suffix}"
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     rec, rec_src = pmc_record(dom_kernel, args.config, log2n, L)
     traffic = None if rec is None else rec.get("hbm_bytes_per_launch")

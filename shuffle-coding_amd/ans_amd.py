@@ -27,6 +27,7 @@ ANS_OK, ANS_E_ZERO_MASS, ANS_E_EXHAUSTED, ANS_E_LEN, ANS_E_SYMBOL = 0, 1, 2, 3, 
 ANS_E_NORM_RANGE, ANS_E_DEVICE, ANS_E_ALLOC, ANS_E_ARG, ANS_E_MISMATCH = 5, 6, 7, 8, 9
 GEN_ZEROS, GEN_EMPTY, GEN_RANDOM = 0, 1, 2
 ANS_PATH_ENC_LDS, ANS_PATH_ENC_GLOBAL, ANS_PATH_DEC_LDS, ANS_PATH_DEC_GLOBAL = 1, 2, 4, 8
+ANS_PATH_ENC_WIDE, ANS_PATH_DEC_WIDE = 16, 32
 MAX_MIN_HEAD = 1 << 56
 MAX_SIZE = MAX_MIN_HEAD >> 10
 
@@ -633,6 +634,8 @@ class GpuTable:
         p = self.paths()
         if p & ANS_PATH_DEC_LDS:
             return "lds"
+        if p & ANS_PATH_DEC_WIDE and sym_bytes > 1:
+            return "wide"
         if p & ANS_PATH_DEC_GLOBAL and sym_bytes > 1:
             return "global"
         return "generic"

@@ -66,6 +66,12 @@ __device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
 
 // s_waitcnt vmcnt(0) (gfx9 encoding; expcnt/lgkmcnt left at their maxima).
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// s_waitcnt vmcnt(N): all but the N youngest vector-memory operations done (in issue order)
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
@@ -102,6 +108,7 @@ __device__ __forceinline__ uint64_t qest_m1(uint64_t x, double rcp) {
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t off) { return *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(off)); }
 __device__ __forceinline__ uint64_t lds_ld64(uint32_t off) { return *reinterpret_cast<const lds_u64*>(static_cast<uintptr_t>(off)); }
 typedef __attribute__((address_space(3))) v4u32 lds_v4u32;
@@ -110,14 +117,17 @@ __device__ __forceinline__ uint4 lds_ld128(uint32_t off) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// at kEncRingBase: a row address is one v_and_or of the row bits and the lane's column
-struct Ring {
+// at kBase (kEncRingBase for the LDS-row encoder): a row address is one v_and_or of the row bits
+// and the lane's column
+template <uint32_t kBase>
+struct RingT {
     uint32_t col;  // 4 * lane
     __device__ __forceinline__ lds_u32& at(int32_t i) const {
         const uint32_t a = ((static_cast<uint32_t>(i) << 11) & 0xF800u) | col;
-        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a + kEncRingBase));
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a + kBase));
     }
 };
+using Ring = RingT<kEncRingBase>;
 
 template <typename Sym>
 __device__ __forceinline__ uint32_t sym_of(const uint4& v, int j) {
@@ -146,7 +156,8 @@ __device__ __forceinline__ void put_sym(uint4& v, int j, uint32_t s) {
 // and stores only dword w (one ds_write_b32).  Dword w+1, when the push reached it, becomes X:
 // the next push (or finish) stores it with its own bytes, before any page holding it completes.
 // Bytes past the new end are garbage that the next push overwrites.
-struct Funnel {
+template <uint32_t kBase>
+struct FunnelT {
     uint32_t X, pos8, neg8, addr, col;  // addr = ring address of dword pos/4 (row | col)
 
     __device__ __forceinline__ void push(uint32_t lo, uint32_t k8) {
@@ -154,7 +165,7 @@ struct Funnel {
         asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
         asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d0) : "v"(lo), "v"(pos8), "v"(xv));
         asm("v_lshrrev_b32 %0, %1, %2" : "=v"(d1) : "v"(neg8), "v"(lo));
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase)) = d0;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kBase)) = d0;
         pos8 += k8;
         neg8 -= k8;
         const uint32_t a = ((pos8 << 6) & 0xF800u) | col;
@@ -166,12 +177,13 @@ struct Funnel {
     __device__ __forceinline__ void finish() {
         uint32_t xv;
         asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kEncRingBase)) = xv;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kBase)) = xv;
     }
 };
+using Funnel = FunnelT<kEncRingBase>;
 
-template <bool kNT = false>
-__device__ __forceinline__ void flush_page(const Ring& ring, uint32_t p, uint8_t* dst) {
+template <bool kNT = false, uint32_t kBase = kEncRingBase>
+__device__ __forceinline__ void flush_page(const RingT<kBase>& ring, uint32_t p, uint8_t* dst) {
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = ring.at(static_cast<int32_t>(16 * p + i));

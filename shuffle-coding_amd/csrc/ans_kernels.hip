@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "ans_ctx.hpp"
+#include "ans_wide.hpp"
 
 namespace {
 
@@ -477,7 +478,16 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         default: if (k32) ENC(4, true, G, R); else ENC(4, false, G, R); break; \
         }
         if constexpr (sizeof(Sym) > 1) {
-            if (ft.enc_global) {
+            if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
+                const size_t wlds = fast::kWideEncCum + 4 * (ft.enc_nl + 1);
+#define ENCW(KM, K32) fast::k_encode_w<Sym, KM, K32><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
+                switch (ft.kmax) {
+                case 1: case 2: if (k32) ENCW(2, true); else ENCW(2, false); break;
+                case 3: if (k32) ENCW(3, true); else ENCW(3, false); break;
+                default: if (k32) ENCW(4, true); else ENCW(4, false); break;
+                }
+#undef ENCW
+            } else if (ft.enc_global) {
                 ENC_KMAX(true, false)
             } else if (ft.enc_rare) {
                 ENC_KMAX(false, true)
@@ -527,8 +537,12 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         constexpr int U = 16 / sizeof(Sym);
         if (global_table) {
-            if constexpr (sizeof(Sym) > 1)
-                fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+            if constexpr (sizeof(Sym) > 1) {
+                if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0 && slot_cap % 128 == 0)
+                    fast::k_decode_w<Sym><<<grid, fast::kBlock, 160 * 1024, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+                else
+                    fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+            }
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
@@ -712,6 +726,59 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         }
     }
     ft.dec_global = !ft.dec_usable;
+    ft.enc_wide = ft.enc_global && t.norm >= fast::kWideNormMin;
+    ft.enc_nl = std::min<uint32_t>(nsym, fast::kWideEncCumMax - 1);
+    // k_decode_w's LDS prefix: for each bucket width 2^shp, the longest prefix of symbols whose
+    // bucket starts (u16) and cdf fit beside the ring; keep the width whose prefix covers the most
+    // probability among those whose cf needs a fifth candidate at most 0.1% of the time
+    std::vector<uint16_t> wide_s0;
+    if (ft.dec_global && nsym <= 65536) {
+        const uint32_t budget = fast::kWideDecTabBytes;
+        uint32_t best_shp = 0, best_nlp = 0;
+        uint64_t best_cov = 0;
+        double best_far = 2.0;
+        for (uint32_t shp = 0; shp <= 24; ++shp) {
+            auto bytes = [&](uint32_t nlp) {
+                const uint64_t nbp = nlp ? ((static_cast<uint64_t>(cum[nlp]) + (1ull << shp) - 1) >> shp) : 0;
+                return ((2 * nbp + 15) & ~uint64_t(15)) + 4ull * (nlp + 6);
+            };
+            uint32_t lo = 0, hi = nsym;  // largest nlp with bytes(nlp) <= budget (bytes grows with nlp)
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (bytes(mid) <= budget) lo = mid;
+                else hi = mid - 1;
+            }
+            const uint32_t nlp = lo;
+            if (nlp == 0 || cum[nlp] == 0) continue;
+            const uint64_t cpre = cum[nlp], nbp = (cpre + (1ull << shp) - 1) >> shp;
+            uint64_t far = 0;  // cf values of the prefix past their bucket's fifth candidate
+            for (uint64_t b = 0; b < nbp; ++b) {
+                const uint64_t a = b << shp, e = std::min<uint64_t>(cpre, (b + 1) << shp);
+                const uint64_t s0 = cat.icdf(a).first;
+                const uint64_t c4 = s0 + 4 <= nsym ? cum[s0 + 4] : t.norm;
+                if (c4 < e) far += e - std::max<uint64_t>(a, c4);
+            }
+            const double far_frac = static_cast<double>(far) / static_cast<double>(cpre);
+            const bool ok = far_frac <= 1e-3, best_ok = best_far <= 1e-3;
+            if ((ok && (!best_ok || cpre > best_cov)) || (!ok && !best_ok && far_frac < best_far)) {
+                best_shp = shp;
+                best_nlp = nlp;
+                best_cov = cpre;
+                best_far = far_frac;
+            }
+        }
+        if (best_nlp > 0) {
+            ft.dec_wide = 1;
+            ft.dec_w_shp = best_shp;
+            ft.dec_w_nlp = best_nlp;
+            ft.dec_w_cpre = cum[best_nlp];
+            ft.dec_w_nbp = static_cast<uint32_t>((static_cast<uint64_t>(ft.dec_w_cpre) + (1ull << best_shp) - 1) >> best_shp);
+            ft.dec_w_cum_off = (2 * ft.dec_w_nbp + 15) & ~15u;
+            wide_s0.resize(ft.dec_w_nbp + 2, 0);
+            for (uint32_t b = 0; b < ft.dec_w_nbp; ++b)
+                wide_s0[b] = static_cast<uint16_t>(cat.icdf(static_cast<uint64_t>(b) << best_shp).first);
+        }
+    }
     ft.nsym = nsym;
     ft.enc_rows = nsym + 1;
     ft.dec_buckets = nb;
@@ -731,9 +798,11 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const size_t decg_b = sizeof(DecBucketG) * decg.size();
     const size_t o_dec = (enc_b + 255) & ~size_t(255), o_cum = o_dec + ((dec_b + 255) & ~size_t(255));
     const size_t o_decg = o_cum + ((sizeof(uint32_t) * cum.size() + 255) & ~size_t(255));
+    const size_t o_ws0 = o_decg + ((decg_b + 255) & ~size_t(255));
+    const size_t ws0_b = sizeof(uint16_t) * wide_s0.size();
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
-    HIP_TRY(hipMalloc(&mem, o_decg + decg_b));
+    HIP_TRY(hipMalloc(&mem, o_ws0 + ws0_b + 16));
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
@@ -748,6 +817,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     }
     HIP_TRY(hipMemcpy(base + o_cum, cum.data(), sizeof(uint32_t) * cum.size(), hipMemcpyHostToDevice));
     if (decg_b) HIP_TRY(hipMemcpy(base + o_decg, decg.data(), decg_b, hipMemcpyHostToDevice));
+    if (ws0_b) HIP_TRY(hipMemcpy(base + o_ws0, wide_s0.data(), ws0_b, hipMemcpyHostToDevice));
+    ft.dec_w_s0 = reinterpret_cast<const uint16_t*>(base + o_ws0);
     ft.dbkt_g = reinterpret_cast<const DecBucketG*>(base + o_decg);
     ft.enc = reinterpret_cast<const EncRow*>(base);
     ft.dbkt = reinterpret_cast<const DecBucket*>(base + o_dec);
@@ -1515,6 +1586,8 @@ int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
     if (ft.usable) p |= ft.enc_global ? ANS_PATH_ENC_GLOBAL : ANS_PATH_ENC_LDS;
     if (ft.usable && ft.dec_usable) p |= ANS_PATH_DEC_LDS;
     if (ft.usable && ft.dec_global) p |= ANS_PATH_DEC_GLOBAL;
+    if (ft.usable && ft.enc_wide) p |= ANS_PATH_ENC_WIDE;
+    if (ft.usable && ft.dec_wide) p |= ANS_PATH_DEC_WIDE;
     *paths = p;
     return ANS_OK;
 }

@@ -1,0 +1,447 @@
+// ans_wide.hpp — fast kernels for large alphabets (nsym > 256: C4's 65,536-symbol table).
+//
+// Same messages and bytes as ans_fast.hpp (one lane = one chunk = one reference Message:
+// src/ans.rs:292 zeros, src/codec.rs:415-424 IID, src/ans.rs:96-116 push/pop,
+// src/ans.rs:255-264 flatten/unflatten); what differs is where the table lives.  A table of
+// 65,536 rows does not fit in LDS, and a random 4-16 B gather from the L2 costs one L2 request
+// whatever its width: tools/l2rand.hip measures ~265-300 G lane-requests/s chip-wide for
+// tables of 256 KiB-2 MiB (any load width, any cache-policy bit), i.e. a whole 128-B line
+// per request.  So these kernels cut L2 requests per symbol:
+//  * the table is the bare cdf array (u32 cdf(0..nsym+5), 256 KiB for C4): a symbol's row is
+//    the 8-B pair (cdf(s), cdf(s+1)), one request, and the smaller array keeps more of itself
+//    in each CU's 32-KiB L1;
+//  * the LDS holds a prefix of that array beside the byte ring, so every symbol below the
+//    prefix bound (37% of C4's symbols in the encoder, ~24% of its probability in the
+//    decoder) never leaves the CU;
+//  * the encoder forms 1/p from v_rcp_f64 plus one Newton step instead of reading it
+//    (error <= 2^-44 relative: the quotient estimate of DESIGN.md §4 holds for norm >= 2^22);
+//  * streams move 128 B per lane per global access (aligned page pairs): a 128-B L2 line is
+//    fetched once instead of once per 64-B half (profiles/r02_hbm_calib.txt).
+#pragma once
+
+#include "ans_fast.hpp"
+
+namespace shuffle_coding {
+namespace fast {
+
+// ---- encoder LDS: the byte ring at offset 0 (64 KiB, 512 lanes), the cdf prefix after it
+constexpr uint32_t kWideRing = 0;
+constexpr uint32_t kWideEncCum = kEncRingBytes;
+constexpr uint32_t kWideEncCumMax = (160u * 1024u - kWideEncCum) / 4u;  // staged cdf entries
+constexpr uint32_t kWideNormMin = 1u << 22;  // one Newton step suffices above (see k_encode_w)
+
+typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
+
+// (cdf(s), cdf(s+1)) from the global cdf array: one 8-B load at a 4-B aligned address
+__device__ __forceinline__ v2u32 cum_pair_global(const uint32_t* cum, uint32_t s) {
+    typedef __attribute__((address_space(1))) const v2u32 gv2;
+    return *reinterpret_cast<gv2*>(reinterpret_cast<uintptr_t>(cum + s));
+}
+// ... and from the LDS prefix (ds_read2_b32: any dword alignment)
+__device__ __forceinline__ v2u32 cum_pair_lds(uint32_t base, uint32_t s) {
+    const lds_u32* p = reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(base + 4 * s));
+    return v2u32{p[0], p[1]};
+}
+
+// fl(1/p) to within 2^-44 relative: v_rcp_f64 (tools/rcp_check.hip measures up to 2^28 ulp,
+// ~2^-24 relative) and one Newton step r' = r + r(1 - p r), whose error is the square of that
+// plus two roundings.  With x < 2^64 and norm >= 2^22, x/p < 2^42, so the estimate of
+// qest_m1 stays within 2^42 * (2^-44 + 2^-52) < 1/2 of x/p: q_m in {q - 1, q} as before.
+__device__ __forceinline__ double rcp_newton(uint32_t p) {
+    const double d = static_cast<double>(p);
+    const double r = __builtin_amdgcn_rcp(d);
+    const double e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// Encoder for nsym > 256 (u16 / u32 symbols): rows from the LDS prefix or the global cdf.
+// Groups of 128 B of symbols (8 units of 16 B) per lane, walked last to first; each unit's rows
+// are requested at the point before it (LDS or global, per lane), so their latency hides behind
+// one unit of work.  Points and the byte funnel are ans_fast.hpp's.
+template <typename Sym, int KMAX, bool kK32>
+__global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
+                                                         uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                         uint32_t* __restrict__ lens, uint32_t* __restrict__ status) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    {
+        uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideEncCum);
+        for (uint32_t i = threadIdx.x; i <= t.enc_nl; i += kBlock) lc[i] = t.cum[i];
+    }
+    const RingT<kWideRing> ring{4 * threadIdx.x};
+    __syncthreads();
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= nfull) return;
+
+    constexpr int U = 16 / static_cast<int>(sizeof(Sym));
+    constexpr int GU = 8;  // units per 128-B group
+    const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
+    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
+    uint8_t* dst = slots + c * slot_cap;
+    const uint32_t npages_cap = static_cast<uint32_t>(slot_cap / 64);
+    const uint64_t K = t.K;
+    const uint32_t norm = t.norm;
+    const uint32_t nsym = t.nsym;  // out-of-range symbols read the zero-mass pair (cdf(nsym), cdf(nsym+1))
+    const uint32_t nl = t.enc_nl;
+    const uint32_t exp_norm = 0x43300000u * norm;
+    const uint32_t* gcum = t.cum;
+
+    uint64_t head = kMaxMinHead;  // Message::zeros()
+    FunnelT<kWideRing> f{0, 0, 0, ring.col, ring.col};
+    uint32_t fp = 0, over = 0;
+    uint32_t minmass = ~0u;
+
+    auto flush = [&]() __attribute__((always_inline)) {
+        if ((f.pos8 >> 9) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
+            if (fp < npages_cap) flush_page<false, kWideRing>(ring, fp, dst);
+            else over = 1;
+            ++fp;
+        }
+    };
+    // a unit's rows: every lane reads the LDS pair of min(s, nl) (always in range) and the lanes
+    // whose symbol lies past the prefix also load the global pair, into separate registers (a
+    // shared destination would make each LDS read wait for every outstanding global load)
+    auto request = [&](const uint4& unit, v2u32* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t s = min(sym_of<Sym>(unit, j), nsym);
+            lbuf[j] = cum_pair_lds(kWideEncCum, min(s, nl));
+            if (s >= nl) gbuf[j] = cum_pair_global(gcum, s);
+        }
+    };
+    // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
+    auto bytes_out8 = [&](uint64_t pK) __attribute__((always_inline)) {
+        uint32_t k = (head >> 8) >= pK ? 8u : 0u;
+        if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 8u : 0u;
+        if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 8u : 0u;
+        if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 8u : 0u;
+        return k;
+    };
+    auto process = [&](const uint4& unit, const v2u32* lbuf, const v2u32* gbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
+            const bool in_lds = min(sym_of<Sym>(unit, j), nsym) < nl;
+            const v2u32 row = in_lds ? lbuf[j] : gbuf[j];
+            const uint32_t cum = row.x, p = row.y - row.x;  // cdf(x), pmf(x) (src/codec.rs:63-64)
+            asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(p));
+            const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
+            const uint32_t k8 = bytes_out8(pK);
+            f.push(lo32(head), k8);
+            head >>= k8;
+            // q = head / p, r = head % p (src/ans.rs:101-102), head = norm*q + cdf(x, r)
+            // (src/ans.rs:103-104): ans_fast.hpp push_one's form, with 1/p from rcp_newton
+            const uint64_t qb = qest_m1(head, rcp_newton(p));
+            const uint32_t rm = lo32(head) - lo32(qb) * p;
+            const uint32_t a = cum + rm + (rm >= p ? norm - p : 0u);
+            const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * norm + a;
+            uint32_t hq;
+            asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb)), "s"(norm));
+            head = mk64(hi32(lo64) + hq - exp_norm, lo32(lo64));
+        }
+    };
+
+    uint4 n[GU];
+    {
+        const uint4* gsrc = src + GU * (ngroups - 1);
+#pragma unroll
+        for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
+    }
+    v2u32 la[U], lb[U], ga[U], gb[U];
+    wait_vm();
+    request(n[GU - 1], la, ga);
+    for (int g = ngroups - 1; g >= 0; --g) {
+        uint4 cc[GU];
+#pragma unroll
+        for (int i = 0; i < GU; ++i) cc[i] = n[i];
+#pragma unroll
+        for (int u = GU - 1; u >= 0; --u) {
+            // point: the rows of unit u (requested one unit ago) have landed; the group prefetch
+            // issued after them at u = GU-1 may stay in flight through the next point
+            if (u == GU - 2) wait_vm_n<GU>();
+            else wait_vm();
+            flush();
+            const bool odd = (u & 1) != 0;
+            if (u > 0) request(cc[u - 1], odd ? lb : la, odd ? gb : ga);
+            if (u == GU - 1) {
+                const uint4* gsrc = src + GU * (g > 0 ? g - 1 : 0);
+#pragma unroll
+                for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
+            }
+            if (u == 0) request(n[GU - 1], la, ga);  // unit GU-1 of group g-1 (landed units ago)
+            process(cc[u], odd ? la : lb, odd ? ga : gb);
+        }
+    }
+    wait_vm();
+    flush();  // the last unit's completed page: the flatten's 8 bytes may reach the ring slot it holds
+
+    // flatten (src/ans.rs:255-260): all significant head bytes, low first (7 or 8 here)
+    const uint32_t nb = (71u - static_cast<uint32_t>(__builtin_clzll(head))) >> 3;
+    f.push(lo32(head), 32);
+    f.push(hi32(head), 8 * (nb - 4));
+    f.finish();
+    const uint32_t len = f.len();
+    for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
+        if (fp < npages_cap) flush_page<false, kWideRing>(ring, fp, dst);
+        else over = 1;
+    }
+    if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
+        uint32_t sym_err = 0;
+        for (uint64_t k = 0; k < chunk_len; ++k)
+            sym_err |= static_cast<uint32_t>(syms[c * chunk_len + k]) >= t.nsym ? 1u : 0u;
+        atomicOr(status, 1u << (sym_err ? ANS_E_SYMBOL : ANS_E_ZERO_MASS));
+    }
+    if (over) atomicOr(status, 1u << ANS_E_LEN);
+    lens[c] = (over || minmass == 0) ? 0u : len;
+}
+
+// ====================================================================== decode, large alphabets
+// One chain per lane as in ans_fast.hpp k_decode; the icdf (src/codec.rs:65-68) splits by cf:
+//  * cf < cpre = cdf(nlp) (a prefix of the alphabet staged in LDS): bucket cf >> shp gives
+//    s0 = icdf(bucket start) from a u16 array, then cdf(s0..s0+4) from the staged cdf prefix
+//    (three ds_read2_b32) resolve four candidates; cf >= cdf(s0+4) scans the staged cdf (voted);
+//  * otherwise the global DecBucketG of cf >> dec_shift (cdf(s0..s0+5) and s0, 32 B in one
+//    128-B line: one L2 request), with the global cdf scan past its fifth candidate (voted).
+// The stream ring holds two 64-B pages per lane (33 rows x 512 lanes, row 32 mirroring row 0);
+// the next aligned 128-B page pair waits in registers and lands one page per point.  A point
+// comes every 16 symbols (at most 64 B, KMAX <= 4), so reads never reach an unlanded page, and
+// one global page fetch per 128 B exposes its HBM latency once per ~64 symbols (gfx9 retires
+// vector-memory operations in issue order, so a page fetch delays the next bucket load).
+constexpr int kWideDecRows = 33;
+constexpr uint32_t kWideDecTab = kWideDecRows * kBlock * 4;  // 67,584 B of ring, then the tables
+static_assert(kWideDecTab % 256 == 0, "table base");
+constexpr uint32_t kWideDecTabBytes = 160u * 1024u - kWideDecTab;
+__device__ const uint4 kZeroPair[8] = {};  // 128 zero bytes: pages below the stream start
+
+struct DecChainW {
+    uint32_t col;  // 4 * lane
+    const uint8_t* src;
+    uint4 Q[8];    // the page pair (2m, 2m+1) not yet landed
+    int32_t low, P;
+    uint32_t wx, wy, W;
+    uint64_t head;
+    uint64_t qq;
+    uint32_t cf, cum, nxt, sx;
+    bool far;
+
+    __device__ __forceinline__ lds_u32& row(int32_t r) const {
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(static_cast<uint32_t>(r) * (kBlock * 4) + col));
+    }
+    __device__ __forceinline__ void fetch_pair(int32_t m) {
+        typedef __attribute__((address_space(1))) const v4u32 gv4;
+        const uint4* g = m >= 0 ? reinterpret_cast<const uint4*>(src + 128ll * m) : kZeroPair;
+        const gv4* gg = reinterpret_cast<const gv4*>(reinterpret_cast<uintptr_t>(g));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const v4u32 v = gg[k];
+            Q[k] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    }
+    // page p (its half of Q) into ring slot p & 1
+    __device__ __forceinline__ void land(int32_t p) {
+        const int32_t r0 = (p & 1) * 16;
+        if (p & 1) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                row(r0 + 4 * k + 0) = Q[4 + k].x;
+                row(r0 + 4 * k + 1) = Q[4 + k].y;
+                row(r0 + 4 * k + 2) = Q[4 + k].z;
+                row(r0 + 4 * k + 3) = Q[4 + k].w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                row(r0 + 4 * k + 0) = Q[k].x;
+                row(r0 + 4 * k + 1) = Q[k].y;
+                row(r0 + 4 * k + 2) = Q[k].z;
+                row(r0 + 4 * k + 3) = Q[k].w;
+            }
+            row(32) = Q[0].x;
+        }
+    }
+    __device__ __forceinline__ void read_window() {
+        const uint32_t a = ((static_cast<uint32_t>(P) << 9) & 0xF800u) | col;  // row (P >> 2) & 31
+        wy = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a));
+        wx = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a + kBlock * 4));
+    }
+    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
+    // the top two pages land before decoding starts; the pair below them is requested
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
+        src = s;
+        const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
+        fetch_pair(len > 0 ? top >> 1 : -1);
+        wait_vm();
+        land(top);
+        if (top & 1) {
+            land(top - 1);
+            fetch_pair((top >> 1) - 1);  // holds top-3, top-2
+        } else {
+            fetch_pair((top >> 1) - 1);  // holds top-2, top-1
+            wait_vm();
+            land(top - 1);                // top-2 stays in the low half
+        }
+        low = top - 1;
+        P = len - 4;
+        read_window();
+        head = 0;
+    }
+    __device__ __forceinline__ void pull_until(uint64_t bound) {
+        for (int g = 0; g < 9 && head < bound; ++g) {
+            form_window();
+            head = (head << 8) | (W >> 24);
+            P -= 1;
+            read_window();
+        }
+    }
+    // at a point (after s_waitcnt vmcnt(0)): land page low-1 once page low+1 is no longer read
+    __device__ __forceinline__ void point() {
+        if ((((P >> 2) + 1) >> 4) <= low) {
+            land(low - 1);
+            --low;
+            if (!(low & 1)) fetch_pair((low >> 1) - 1);  // the next page (low-1, odd) opens a new pair
+        }
+    }
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
+        form_window();
+        P -= static_cast<int32_t>(renorm_up(head, W, L, hL8));
+        read_window();  // for the next step; kept ahead of this step's lookups
+        __builtin_amdgcn_sched_barrier(0);
+        div_norm(head, norm, rcp_norm, qq, cf);
+    }
+    __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
+};
+
+template <typename Sym>
+__global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
+                                                         uint64_t slot_cap, const uint32_t* __restrict__ lens,
+                                                         uint64_t chunk_len, uint64_t nfull, int gen_kind,
+                                                         Sym* __restrict__ out, uint32_t* __restrict__ status) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    {  // the prefix tables: bucket s0 values (u16), then cdf(0 .. nlp + 5)
+        const uint32_t* gs = reinterpret_cast<const uint32_t*>(t.dec_w_s0);
+        uint32_t* ls = reinterpret_cast<uint32_t*>(lds + kWideDecTab);
+        for (uint32_t i = threadIdx.x; i < (t.dec_w_nbp + 1) / 2; i += kBlock) ls[i] = gs[i];
+        uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideDecTab + t.dec_w_cum_off);
+        for (uint32_t i = threadIdx.x; i <= t.dec_w_nlp + 5; i += kBlock) lc[i] = t.cum[i];
+    }
+    __syncthreads();
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= nfull) return;  // no barrier below: lanes are independent
+    if (lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
+        atomicOr(status, 1u << ANS_E_LEN);
+        return;
+    }
+
+    constexpr int U = 16 / static_cast<int>(sizeof(Sym));
+    constexpr int UPT = 16 / U;  // units per point: 16 symbols, at most 64 stream bytes
+    const int nblocks = static_cast<int>(chunk_len / (4 * U));  // 64 B of symbols per store
+    const uint64_t L = t.L;
+    const uint32_t hL8 = renorm_screen(L);
+    const uint32_t norm = t.norm;
+    const double rcp_norm = t.rcp_norm;
+    const uint32_t shift = t.dec_shift, shp = t.dec_w_shp, cpre = t.dec_w_cpre;
+    const uint32_t lcum = kWideDecTab + t.dec_w_cum_off;  // LDS byte address of cdf(0)
+    const DecBucketG* __restrict__ bkt = t.dbkt_g;
+    const uint32_t* __restrict__ gcum = t.cum;
+    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
+
+    DecChainW ch;
+    ch.col = 4 * threadIdx.x;
+    ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
+    ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
+
+    auto step = [&]() __attribute__((always_inline)) {
+        ch.renorm_div(L, hL8, norm, rcp_norm);
+        const uint32_t cf = ch.cf;
+        const bool pre = cf < cpre;
+        // global bucket (lanes past the prefix only): issued first, the longer round trip
+        uint4 ga = make_uint4(0, 0, 0, 0), gb = make_uint4(0, 0, 0, 0);
+        if (!pre) {
+            const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
+            ga = e[0];
+            gb = e[1];  // c0..c3 | c4, c5, s0, -
+        }
+        // LDS prefix (every lane; the bucket index clamped into the prefix)
+        const uint32_t bi = min(cf, cpre - 1) >> shp;
+        const uint32_t s0 = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(kWideDecTab + 2 * bi));
+        const uint32_t a0 = lcum + 4 * s0;
+        const uint32_t c0 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0));
+        const uint32_t c1 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 4));
+        const uint32_t c2 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 8));
+        const uint32_t c3 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 12));
+        const uint32_t c4 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 16));
+        uint32_t cum, nxt, sx;
+        bool far;
+        if (pre) {
+            const bool b1 = cf >= c1, b2 = cf >= c2, b3 = cf >= c3;
+            cum = b3 ? c3 : (b2 ? c2 : (b1 ? c1 : c0));
+            nxt = b3 ? c4 : (b2 ? c3 : (b1 ? c2 : c1));
+            sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
+            far = cf >= c4;
+        } else {
+            asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w), "v"(gb.x), "v"(gb.y), "v"(gb.z));
+            const bool b1 = cf >= ga.y, b2 = cf >= ga.z, b3 = cf >= ga.w, b4 = cf >= gb.x;
+            cum = b4 ? gb.x : (b3 ? ga.w : (b2 ? ga.z : (b1 ? ga.y : ga.x)));
+            nxt = b4 ? gb.y : (b3 ? gb.x : (b2 ? ga.w : (b1 ? ga.z : ga.y)));
+            sx = gb.z + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
+            far = cf >= gb.y;
+        }
+        if (__builtin_expect(__any(far), 0)) {
+            if (far) {  // more boundaries than candidates: scan the cdf (src/codec.rs:66 partition_point)
+                sx += 1;
+                if (pre) {
+                    while (cf >= *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(lcum + 4 * (sx + 1)))) ++sx;
+                    cum = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(lcum + 4 * sx));
+                    nxt = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(lcum + 4 * (sx + 1)));
+                } else {
+                    while (cf >= gcum[sx + 1]) ++sx;
+                    cum = gcum[sx];
+                    nxt = gcum[sx + 1];
+                }
+            }
+        }
+        ch.cum = cum;
+        ch.nxt = nxt;
+        ch.update();  // head = p*q + r (src/ans.rs:113-114)
+        return sx;
+    };
+
+    uint4 q[4];
+    for (int b = 0; b < nblocks; ++b) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u % UPT == 0) {
+                wait_vm();  // point: retire what the previous point issued
+                if (u == 0 && b > 0) {  // 64 contiguous bytes of symbols per lane
+                    uint4* d = dst + 4 * (b - 1);
+                    d[0] = q[0];
+                    d[1] = q[1];
+                    d[2] = q[2];
+                    d[3] = q[3];
+                }
+                ch.point();
+            }
+            uint4 outv = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                __builtin_amdgcn_sched_barrier(0);
+                put_sym<Sym>(outv, j, step());
+            }
+            q[u] = outv;
+        }
+    }
+    wait_vm();
+    if (nblocks > 0) {
+        uint4* d = dst + 4 * (nblocks - 1);
+        d[0] = q[0];
+        d[1] = q[1];
+        d[2] = q[2];
+        d[3] = q[3];
+    }
+    // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
+    ch.pull_until(kMaxMinHead);
+    const int32_t remaining = ch.P + 4;  // < 0: generated
+    if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
+    else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+}
+
+}  // namespace fast
+}  // namespace shuffle_coding

@@ -614,3 +614,59 @@ def test_var_chunks_bit_exact(gpu, which, multiset_masses):
         assert got == want, c
     back = gt.decode_var_chunks(data, offsets, lens, starts, dtype)
     assert np.array_equal(back, syms.astype(dtype))
+
+
+# ---------------------------------------------------------------- large alphabets (ans_wide.hpp)
+def _wide_table(rng, nsym, lo, hi, ones=0, zeros=0, crowd=0):
+    masses = rng.integers(lo, hi, size=nsym, dtype=np.int64)
+    if ones:  # mass-1 symbols: pushes of up to four bytes (kmax 4)
+        masses[rng.choice(nsym, ones, replace=False)] = 1
+    if crowd:  # runs of tiny masses: many cdf boundaries in one bucket (the voted scans)
+        for start in rng.choice(nsym - 64, crowd, replace=False):
+            masses[start:start + 40] = rng.integers(1, 4, 40)
+    if zeros:
+        masses[rng.choice(nsym, zeros, replace=False)] = 0
+    return masses.astype(np.uint64)
+
+
+@pytest.mark.parametrize("nsym,lo,hi,ones,zeros,crowd,chunk_len,n", [
+    (65536, 1, 1 << 12, 0, 0, 0, 4096, 600 * 4096 + 77),   # C4's shape, ragged tail
+    (65536, 1, 1 << 12, 300, 500, 20, 4096, 520 * 4096),  # kmax 4, zero masses, crowded buckets
+    (3000, 1 << 10, 1 << 14, 10, 0, 5, 64, 1200 * 64),    # small chunks (one 128-B group)
+    (40000, 1, 1 << 16, 0, 0, 0, 2048, 600 * 2048),      # prefix and global parts both large
+])
+def test_wide_kernels_bit_exact(gpu, nsym, lo, hi, ones, zeros, crowd, chunk_len, n):
+    """The large-alphabet kernels (k_encode_w: cdf-pair rows from the LDS prefix or global
+    memory, 1/p by v_rcp_f64 + Newton; k_decode_w: LDS-prefix icdf + global buckets) against
+    the oracle, symbols drawn from the table so both table parts and the scans are hit."""
+    rng = np.random.default_rng(nsym + n)
+    masses = _wide_table(rng, nsym, lo, hi, ones, zeros, crowd)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    assert gt.paths() & A.ANS_PATH_ENC_WIDE and gt.decode_kernel(2) == "wide"
+    nz = np.flatnonzero(masses)
+    p = masses[nz].astype(np.float64)
+    # half the symbols by probability, half uniform over the non-zero ones (tiny masses too)
+    syms = np.where(rng.random(n) < 0.5, rng.choice(nz, size=n, p=p / p.sum()), rng.choice(nz, size=n))
+    for dtype in (np.uint16, np.uint32):
+        _roundtrip_vs_oracle(gpu, masses, syms.astype(np.uint32), chunk_len, dtype)
+
+
+def test_wide_kernel_errors(gpu):
+    rng = np.random.default_rng(3)
+    masses = _wide_table(rng, 5000, 1 << 10, 1 << 13)
+    masses[1234] = 0
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    assert gt.paths() & A.ANS_PATH_ENC_WIDE
+    syms = rng.integers(0, 5000, size=600 * 4096).astype(np.uint16)
+    syms[syms == 1234] = 1235
+    gt.encode_chunks(syms, 4096)
+    bad = syms.copy()
+    bad[77 * 4096 + 5] = 1234  # zero mass (src/ans.rs:98)
+    with pytest.raises(A.AnsError) as e:
+        gt.encode_chunks(bad, 4096)
+    assert e.value.code == A.ANS_E_ZERO_MASS
+    bad = syms.copy()
+    bad[300 * 4096 + 4095] = 60000  # out of range for a 5000-symbol table (src/codec.rs:63)
+    with pytest.raises(A.AnsError) as e:
+        gt.encode_chunks(bad, 4096)
+    assert e.value.code == A.ANS_E_SYMBOL

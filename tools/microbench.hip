@@ -183,6 +183,20 @@ KERNEL(k_mad64_dep, DECL64, INIT64, OPMADDEP, SINK64)
 KERNEL(k_fma_f64_dep, DECLF, INITF, OPFMAFDEP, SINKF)
 KERNEL(k_perm_dep, DECL32, INIT32, OPPERMDEP, SINK32)
 
+#define RCPF(D, S) asm volatile("v_rcp_f64 %0, %1" : "=v"(D) : "v"(S))
+#define OPRCPF RCPF(d0, d1); RCPF(d1, d2); RCPF(d2, d3); RCPF(d3, d4); RCPF(d4, d5); RCPF(d5, d6); RCPF(d6, d7); RCPF(d7, d0)
+KERNEL(k_rcp_f64, DECLF, INITF, OPRCPF, SINKF)
+#define FRX(D, S) asm volatile("v_frexp_exp_i32_f64 %0, %1" : "=v"(D) : "v"(S))
+KERNEL(k_frexp, DECLF; unsigned e0 = 0, INITF, FRX(e0, d1); FRX(e0, d2); FRX(e0, d3); FRX(e0, d4); FRX(e0, d5); FRX(e0, d6); FRX(e0, d7); FRX(e0, d0), SINKF + e0)
+#define SUBB(D, S) asm volatile("v_sub_co_u32 %0, vcc, %0, %1" : "+v"(D) : "v"(S) : "vcc")
+KERNEL(k_sub_co, DECL32, INIT32, SUBB(a0, a1); SUBB(a1, a2); SUBB(a2, a3); SUBB(a3, a4); SUBB(a4, a5); SUBB(a5, a6); SUBB(a6, a7); SUBB(a7, a0), SINK32)
+KERNEL(k_mul_u32_u24_dep, DECL32, INIT32, OP32("v_mul_u32_u24"), SINK32)
+KERNEL(k_lshlrev_b16, DECL32, INIT32, OP32("v_lshlrev_b16"), SINK32)
+KERNEL(k_add_u16, DECL32, INIT32, OP32("v_add_u16"), SINK32)
+KERNEL(k_cvt_f64_i32, DECLF, INITF, OPCVT, SINKF)
+#define CVTF(D, S) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(D) : "v"(S))
+KERNEL(k_cvt_f32_f64, DECLF; float g0 = 0, INITF, CVTF(g0, d1); CVTF(g0, d2); CVTF(g0, d3); CVTF(g0, d4); CVTF(g0, d5); CVTF(g0, d6); CVTF(g0, d7); CVTF(g0, d0), SINKF + (unsigned)g0)
+
 int main(int argc, char** argv) {
     const int blocks = 256 * (argc > 1 ? atoi(argv[1]) : 8), threads = 256;
     unsigned* out;
@@ -216,6 +230,8 @@ int main(int argc, char** argv) {
         {"v_or3_b32", k_or3_b32, 1}, {"v_bfi_b32", k_bfi_b32, 1}, {"v_lshl_add_u32", k_lshl_add_u32, 1},
         {"DEP v_fma_f32", k_fma_f32_dep, 1}, {"DEP v_add_u32", k_add_u32_dep, 1}, {"DEP v_mad_u64_u32", k_mad64_dep, 1},
         {"DEP v_fma_f64", k_fma_f64_dep, 1}, {"DEP v_perm_b32", k_perm_dep, 1},
+        {"v_rcp_f64", k_rcp_f64, 1}, {"v_frexp_exp_i32_f64", k_frexp, 1}, {"v_sub_co_u32", k_sub_co, 1},
+        {"v_lshlrev_b16", k_lshlrev_b16, 1}, {"v_add_u16", k_add_u16, 1}, {"v_cvt_f32_f64", k_cvt_f32_f64, 1},
     };
     printf("clock(max) %.0f MHz, CUs %d\n", clk_hz / 1e6, prop.multiProcessorCount);
     for (auto& k : ks) {

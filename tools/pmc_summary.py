@@ -20,7 +20,7 @@ import json
 import os
 from collections import defaultdict
 
-KEYS = ("k_encode", "k_decode_g", "k_decode", "k_gen_iid", "k_compact", "k_sample_iid")
+KEYS = ("k_encode_w", "k_encode", "k_decode_g", "k_decode_w", "k_decode", "k_gen_iid", "k_compact", "k_sample_iid")
 
 
 def short(name):
