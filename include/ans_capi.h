@@ -36,7 +36,7 @@ extern "C" {
 /* ---- tail generators: src/ans.rs:131-136 TailGenerator ---- */
 #define ANS_GEN_ZEROS 0  /* Message::zeros()  src/ans.rs:292 */
 #define ANS_GEN_EMPTY 1  /* Message::empty()  src/ans.rs:297 */
-#define ANS_GEN_RANDOM 2 /* Message::random() src/ans.rs:285 (host only; bytes parity-unpinned) */
+#define ANS_GEN_RANDOM 2 /* Message::random() src/ans.rs:285 (PCG bytes parity-unpinned) */
 
 const char *ans_status_string(int status);
 int ans_abi_version(void); /* bumps on any incompatible change */
@@ -155,6 +155,22 @@ int ans_gpu_decode_chunks(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len,
                           const uint64_t *lens, uint64_t n, uint64_t chunk_len, int gen_kind, void *out,
                           int sym_bytes);
 
+/* Chunks from another initial message (the _ex variants of this section): gen_kind = ANS_GEN_ZEROS
+ * (Message::zeros(), what the plain calls use), ANS_GEN_EMPTY (Message::empty(): same bytes, an
+ * exhausted tail is ANS_E_EXHAUSTED on decode) or ANS_GEN_RANDOM (chunk c starts from
+ * Message::random(seed + c), src/ans.rs:285-290: head 1 then seven generator bytes pulled, the
+ * reference harness' initial message, src/multiset.rs:174, src/benchmark.rs:698-700).  A push
+ * never pulls, so a chunk's stream holds no generated byte; decode is
+ * Message::unflatten(m.flatten()) of that message (src/ans.rs:57: the tail keeps its generator
+ * state) and must end back at Message::random(seed + c) (src/ans.rs:56), else ANS_E_MISMATCH.
+ * A corrupt RANDOM stream that reaches past its start is reported, not decoded further. */
+int ans_gpu_encode_chunks_ex(ans_gpu_table *gt, const void *syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                             int gen_kind, uint64_t seed, uint8_t *out, uint64_t out_cap, uint64_t *offsets,
+                             uint64_t *lens, uint64_t *total);
+int ans_gpu_decode_chunks_ex(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
+                             const uint64_t *lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
+                             void *out, int sym_bytes);
+
 /* Device-resident variants: all pointers are device pointers; asynchronous on `stream`
  * (a hipStream_t; NULL = the context's stream).  Streams live in fixed slots: chunk j at
  * d_slots + j*slot_cap (slot_cap from ans_gpu_slot_capacity).  Errors found on the
@@ -166,6 +182,12 @@ int ans_dev_encode_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, 
 int ans_dev_decode_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
                           const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void *d_syms,
                           int sym_bytes, uint32_t *d_status, void *stream);
+int ans_dev_encode_chunks_ex(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                             int gen_kind, uint64_t seed, uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens,
+                             uint32_t *d_status, void *stream);
+int ans_dev_decode_chunks_ex(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
+                             const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
+                             void *d_syms, int sym_bytes, uint32_t *d_status, void *stream);
 /* Synthetic iid symbols, counter-based: symbol i of seed k is
  * icdf(floor(splitmix64((k << 48) ^ (start + i)) * norm / 2^64)). */
 int ans_dev_gen_iid(ans_gpu_table *gt, uint64_t seed, uint64_t start, uint64_t n, void *d_syms, int sym_bytes,
@@ -195,6 +217,19 @@ int ans_gpu_encode_var_chunks(ans_gpu_table *gt, const void *syms, int sym_bytes
 int ans_gpu_decode_var_chunks(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
                               const uint64_t *lens, uint64_t nchunks, const uint64_t *starts, int gen_kind, void *out,
                               int sym_bytes);
+/* ... from the initial messages of the _ex note above (chunk c: Message::random(seed + c)) */
+int ans_dev_encode_var_chunks_ex(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t nchunks,
+                                 const uint64_t *d_starts, int gen_kind, uint64_t seed, uint8_t *d_slots,
+                                 uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status, void *stream);
+int ans_dev_decode_var_chunks_ex(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
+                                 const uint32_t *d_lens, uint64_t nchunks, const uint64_t *d_starts, int gen_kind,
+                                 uint64_t seed, void *d_syms, int sym_bytes, uint32_t *d_status, void *stream);
+int ans_gpu_encode_var_chunks_ex(ans_gpu_table *gt, const void *syms, int sym_bytes, uint64_t nchunks,
+                                 const uint64_t *starts, int gen_kind, uint64_t seed, uint8_t *out, uint64_t out_cap,
+                                 uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_decode_var_chunks_ex(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
+                                 const uint64_t *lens, uint64_t nchunks, const uint64_t *starts, int gen_kind,
+                                 uint64_t seed, void *out, int sym_bytes);
 /* Compacts slot streams into a dense buffer: d_out[d_offsets[j] ..] = slot j. */
 int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const uint32_t *d_lens,
                     const uint64_t *d_offsets, uint64_t nchunks, uint8_t *d_out, void *stream);

@@ -433,7 +433,20 @@ int orc_decode_chunks(const uint64_t *masses, uint32_t nsym, const uint8_t *in, 
     int rc = ORC_OK;
     for (uint64_t j = 0; j < nchunks && rc == ORC_OK; ++j) {
         uint64_t a = j * chunk_len, b = a + chunk_len < n ? a + chunk_len : n;
-        orc_msg *m = orc_msg_unflatten(in + offsets[j], lens[j], kind, seed + j);
+        orc_msg *m;
+        if (kind == GEN_RANDOM) {
+            /* Message::unflatten(m.flatten()) of a message begun as Message::random(seed + j):
+             * the tail keeps its generator state and num_generated (ans.rs:57, 255-264), so
+             * the round trip ends equal to Message::random(seed + j) (ans.rs:56) */
+            m = orc_msg_new(kind, seed + j);
+            if (m && tail_reserve(&m->tail, lens[j] ? lens[j] : 1) == 0) {
+                if (lens[j]) memcpy(m->tail.el, in + offsets[j], lens[j]);
+                m->tail.len = lens[j];
+                m->head = 0;
+            }
+        } else {
+            m = orc_msg_unflatten(in + offsets[j], lens[j], kind, seed + j);
+        }
         rc = orc_iid_pop(m, c, out + a, b - a);
         if (rc == ORC_OK) {
             orc_msg *init = orc_msg_new(kind, seed + j);

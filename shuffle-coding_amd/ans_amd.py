@@ -77,6 +77,14 @@ SIGNATURES = {
     "ans_gpu_table_free": (None, [vp]),
     "ans_gpu_slot_capacity": (ci, [vp, u64, u64p]),
     "ans_gpu_table_paths": (ci, [vp, ctypes.POINTER(ctypes.c_uint32)]),
+    "ans_gpu_encode_chunks_ex": (ci, [vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_decode_chunks_ex": (ci, [vp, vp, u64, vp, vp, u64, u64, ci, u64, vp, ci]),
+    "ans_dev_encode_chunks_ex": (ci, [vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_decode_chunks_ex": (ci, [vp, vp, vp, u64, vp, u64, u64, ci, u64, vp, ci, vp, vp]),
+    "ans_gpu_encode_var_chunks_ex": (ci, [vp, vp, ci, u64, vp, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_decode_var_chunks_ex": (ci, [vp, vp, u64, vp, vp, u64, vp, ci, u64, vp, ci]),
+    "ans_dev_encode_var_chunks_ex": (ci, [vp, vp, ci, u64, vp, ci, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_decode_var_chunks_ex": (ci, [vp, vp, vp, u64, vp, u64, vp, ci, u64, vp, ci, vp, vp]),
     "ans_gpu_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_decode_chunks": (ci, [vp, vp, u64, vp, vp, u64, u64, ci, vp, ci]),
     "ans_dev_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, vp]),
@@ -646,8 +654,9 @@ class GpuTable:
         return c.value
 
     # ---- host buffers
-    def encode_chunks(self, syms, chunk_len):
-        """syms: np array of uint8/16/32.  Returns (dense bytes, offsets u64, lens u64)."""
+    def encode_chunks(self, syms, chunk_len, gen_kind=GEN_ZEROS, seed=0):
+        """syms: np array of uint8/16/32.  Returns (dense bytes, offsets u64, lens u64).  Chunk c
+        starts from Message::zeros() (or Message::random(seed + c) with gen_kind=GEN_RANDOM)."""
         syms = np.ascontiguousarray(syms)
         w = _WIDTH[syms.dtype]
         n = len(syms)
@@ -657,22 +666,22 @@ class GpuTable:
         out = np.empty(max(nchunks * self.slot_capacity(chunk_len), 1), np.uint8)
         offsets = np.zeros(max(nchunks, 1), np.uint64)
         lens = np.zeros(max(nchunks, 1), np.uint64)
-        _check(lib().ans_gpu_encode_chunks(self.h, _np_ptr(syms), w, n, chunk_len, _np_ptr(out), len(out),
-                                           _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
+        _check(lib().ans_gpu_encode_chunks_ex(self.h, _np_ptr(syms), w, n, chunk_len, gen_kind, seed, _np_ptr(out),
+                                              len(out), _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
                "ans_gpu_encode_chunks")
         return out[:total.value], offsets[:nchunks], lens[:nchunks]
 
-    def decode_chunks(self, data, offsets, lens, n, chunk_len, dtype=np.uint32, gen_kind=GEN_ZEROS):
+    def decode_chunks(self, data, offsets, lens, n, chunk_len, dtype=np.uint32, gen_kind=GEN_ZEROS, seed=0):
         data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
         offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
         lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
         out = np.zeros(max(n, 1), dtype)
-        _check(lib().ans_gpu_decode_chunks(self.h, _np_ptr(data) if data.size else None, data.size,
-                                           _np_ptr(offsets), _np_ptr(lens), n, chunk_len, gen_kind, _np_ptr(out),
-                                           _WIDTH[np.dtype(dtype)]), "ans_gpu_decode_chunks")
+        _check(lib().ans_gpu_decode_chunks_ex(self.h, _np_ptr(data) if data.size else None, data.size,
+                                              _np_ptr(offsets), _np_ptr(lens), n, chunk_len, gen_kind, seed,
+                                              _np_ptr(out), _WIDTH[np.dtype(dtype)]), "ans_gpu_decode_chunks")
         return out[:n]
 
-    def encode_var_chunks(self, syms, starts):
+    def encode_var_chunks(self, syms, starts, gen_kind=GEN_ZEROS, seed=0):
         """Variable-length chunks: chunk c = syms[starts[c]:starts[c+1]], one reference message
         each.  Returns (dense bytes, offsets u64, lens u64)."""
         syms = np.ascontiguousarray(syms)
@@ -683,34 +692,36 @@ class GpuTable:
         offsets = np.zeros(max(nchunks, 1), np.uint64)
         lens = np.zeros(max(nchunks, 1), np.uint64)
         total = u64(0)
-        _check(lib().ans_gpu_encode_var_chunks(self.h, _np_ptr(syms), _WIDTH[syms.dtype], nchunks, _np_ptr(starts),
-                                               _np_ptr(out), len(out), _np_ptr(offsets), _np_ptr(lens),
-                                               ctypes.byref(total)), "ans_gpu_encode_var_chunks")
+        _check(lib().ans_gpu_encode_var_chunks_ex(self.h, _np_ptr(syms), _WIDTH[syms.dtype], nchunks, _np_ptr(starts),
+                                                  gen_kind, seed, _np_ptr(out), len(out), _np_ptr(offsets),
+                                                  _np_ptr(lens), ctypes.byref(total)), "ans_gpu_encode_var_chunks")
         return out[:total.value], offsets[:nchunks], lens[:nchunks]
 
-    def decode_var_chunks(self, data, offsets, lens, starts, dtype=np.uint32, gen_kind=GEN_ZEROS):
+    def decode_var_chunks(self, data, offsets, lens, starts, dtype=np.uint32, gen_kind=GEN_ZEROS, seed=0):
         data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
         offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
         lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
         starts = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
         n = int(starts[-1]) if len(starts) else 0
         out = np.zeros(max(n, 1), dtype)
-        _check(lib().ans_gpu_decode_var_chunks(self.h, _np_ptr(data) if data.size else None, data.size,
-                                               _np_ptr(offsets), _np_ptr(lens), len(starts) - 1, _np_ptr(starts),
-                                               gen_kind, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
+        _check(lib().ans_gpu_decode_var_chunks_ex(self.h, _np_ptr(data) if data.size else None, data.size,
+                                                  _np_ptr(offsets), _np_ptr(lens), len(starts) - 1, _np_ptr(starts),
+                                                  gen_kind, seed, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
                "ans_gpu_decode_var_chunks")
         return out[:n]
 
     # ---- device buffers (torch tensors or raw pointers)
-    def dev_encode(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None):
-        _check(lib().ans_dev_encode_chunks(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, _dptr(d_slots), slot_cap,
-                                           _dptr(d_lens), _dptr(d_status), _sptr(stream)), "ans_dev_encode_chunks")
+    def dev_encode(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None,
+                   gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_encode_chunks_ex(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, gen_kind, seed,
+                                              _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_status), _sptr(stream)),
+               "ans_dev_encode_chunks")
 
     def dev_decode(self, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status,
-                   stream=None, gen_kind=GEN_ZEROS):
-        _check(lib().ans_dev_decode_chunks(self.h, _dptr(d_in), _dptr(d_offsets), slot_cap, _dptr(d_lens), n,
-                                           chunk_len, gen_kind, _dptr(d_syms), sym_bytes, _dptr(d_status),
-                                           _sptr(stream)), "ans_dev_decode_chunks")
+                   stream=None, gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_decode_chunks_ex(self.h, _dptr(d_in), _dptr(d_offsets), slot_cap, _dptr(d_lens), n,
+                                              chunk_len, gen_kind, seed, _dptr(d_syms), sym_bytes, _dptr(d_status),
+                                              _sptr(stream)), "ans_dev_decode_chunks")
 
     def sample_chunks(self, seed, n, chunk_len, dtype=np.uint32):
         """Codec::samples in bulk (src/ans.rs:42-44): chunk c = samples(len, seed + c)."""

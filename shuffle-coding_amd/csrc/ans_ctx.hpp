@@ -74,4 +74,4 @@ struct ans_gpu_table {
 // the body of ans_gpu_encode_var_chunks; starts is a host array of nchunks + 1 entries.
 int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                                const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
-                               uint64_t* lens, uint64_t* total);
+                               uint64_t* lens, uint64_t* total, int gen_kind = ANS_GEN_ZEROS, uint64_t seed = 0);

@@ -102,6 +102,52 @@ __device__ __forceinline__ uint64_t qest_m1(uint64_t x, double rcp) {
     return static_cast<uint64_t>(__double_as_longlong(t));  // raw bits: qest - 1 + 0x43300000'00000000
 }
 
+// TailGenerator::Random (src/ans.rs:129-164): rand_pcg 0.3.1 Pcg64Mcg (MCG-128, XSL-RR-64
+// output) seeded by rand_core 0.6 seed_from_u64 (PCG32 expansion), one byte per draw
+// (rand 0.8.5 Standard<u8> = next_u32() as u8 = next_u64() as u8).  The same restatement as
+// the host's (ans_core.hpp TailGenerator), so GPU samples equal the host's; no reference test
+// pins these bytes (parity unpinned).
+struct Pcg64Mcg {
+    uint64_t lo, hi;
+    __device__ __forceinline__ void seed_from_u64(uint64_t st) {
+        uint32_t w[4];
+        for (int c = 0; c < 4; ++c) {
+            st = st * 6364136223846793005ull + 11634580027462260723ull;
+            const uint32_t xs = static_cast<uint32_t>(((st >> 18) ^ st) >> 27);
+            const uint32_t rot = static_cast<uint32_t>(st >> 59);
+            w[c] = (xs >> rot) | (xs << ((32 - rot) & 31));
+        }
+        lo = (static_cast<uint64_t>(w[1]) << 32 | w[0]) | 3;  // Mcg128Xsl64::new: state | 3
+        hi = static_cast<uint64_t>(w[3]) << 32 | w[2];
+    }
+    __device__ __forceinline__ uint32_t next_byte() {
+        constexpr uint64_t ML = 0x4385DF649FCCF645ull, MH = 0x2360ED051FC65DA4ull;
+        const uint64_t nlo = lo * ML;
+        hi = __umul64hi(lo, ML) + lo * MH + hi * ML;
+        lo = nlo;
+        const uint32_t rot = static_cast<uint32_t>(hi >> 58);
+        const uint64_t xsl = hi ^ lo;
+        return static_cast<uint32_t>((xsl >> rot) | (xsl << ((64 - rot) & 63))) & 0xFFu;
+    }
+};
+
+// A chunk's initial message (include/ans_capi.h ans_*_ex): Message::zeros() / empty() (head
+// 2^56, src/ans.rs:292-299) or Message::random(seed + c) (head 1 then renorm_up(MAX_MIN_HEAD)
+// pulls seven generator bytes, src/ans.rs:285-290).  A push never pulls (head >= norm*K >= p*K),
+// so a chunk's stream holds no generated byte and decoding ends back at this head.
+struct ChunkInit {
+    int kind;
+    uint64_t seed;
+    __device__ __forceinline__ uint64_t head(uint64_t c) const {
+        if (kind != ANS_GEN_RANDOM) return 1ull << 56;
+        Pcg64Mcg r;
+        r.seed_from_u64(seed + c);
+        uint64_t h = 1;
+        while (h < (1ull << 56)) h = (h << 8) | r.next_byte();
+        return h;
+    }
+};
+
 // Lane-private ring of 32 dwords in a [dword][lane] image.
 // LDS accesses by byte offset (address space 3): keeps the address arithmetic in 32 bits
 // where the compiler otherwise adds the (zero) LDS base or splits constants out of offsets.
@@ -209,7 +255,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                                                                          uint64_t chunk_len, uint64_t nfull,
                                                                          uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                                          uint32_t* __restrict__ lens,
-                                                                         uint32_t* __restrict__ status) {
+                                                                         uint32_t* __restrict__ status, ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
     // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
@@ -264,7 +310,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     const uint32_t sentinel = t.enc_rows - 1;  // zero-mass row: out-of-range symbols land here
     const uint32_t exp_norm = 0x43300000u * static_cast<uint32_t>(t.norm);  // qest_m1's exponent word x norm
 
-    uint64_t head = kMaxMinHead;  // Message::zeros()
+    uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
     Funnel f{0, 0, 0, ring.col, ring.col};
     uint32_t fp = 0, over = 0;
     uint32_t minmass = ~0u;  // 0 after a zero-mass / out-of-range symbol; accumulated by an
@@ -646,7 +692,7 @@ template <typename Sym, int SPP, bool kFar, bool kP24, bool kJ4>
 __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
-                                                      uint32_t* __restrict__ status) {
+                                                      uint32_t* __restrict__ status, ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     unsigned char* tab = lds;  // tables at offset 0, ring after them
     {
@@ -720,11 +766,11 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
         d[2] = q2;
         d[3] = q3;
     }
-    // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
+    // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
     const int32_t remaining = ch.P + 4;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
-    else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+    else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
 
 // ====================================================================== decode, large alphabets
@@ -860,7 +906,8 @@ template <typename Sym>
 __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8_t* __restrict__ slots,
                                                         uint64_t slot_cap, const uint32_t* __restrict__ lens,
                                                         uint64_t chunk_len, uint64_t nfull, int gen_kind,
-                                                        Sym* __restrict__ out, uint32_t* __restrict__ status) {
+                                                        Sym* __restrict__ out, uint32_t* __restrict__ status,
+                                                        ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;  // no barrier below: lanes are independent
@@ -920,7 +967,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
     ch.pull_until(kMaxMinHead);
     const int32_t remaining = ch.P + 4;
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
-    else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+    else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
 
 }  // namespace fast

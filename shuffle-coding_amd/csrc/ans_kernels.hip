@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __rest
                                                    uint64_t c_first, uint64_t nchunks,
                                                    uint8_t* __restrict__ slots,
                                                    uint64_t slot_cap, uint32_t* __restrict__ lens,
-                                                   uint32_t* __restrict__ status) {
+                                                   uint32_t* __restrict__ status, fast::ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     const DevSym* rows = t.sym;
     if constexpr (kLds) {
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(DevTable t, const Sym* __rest
     const uint64_t a = starts ? starts[c] : c * chunk_len;
     const uint64_t b = starts ? starts[c + 1] : min(a + chunk_len, n);
     ByteSink sink{slots + c * slot_cap, slot_cap, 0, 0, 0, false};
-    uint64_t head = kMaxMinHead;  // Message::zeros()
+    uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
     const uint64_t norm = t.norm, K = t.K;
     for (uint64_t k = b; k > a;) {
         --k;
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
                                                    const uint32_t* __restrict__ lens, uint64_t n, uint64_t chunk_len,
                                                    const uint64_t* __restrict__ starts,
                                                    uint64_t c_first, uint64_t nchunks, int gen_kind, Sym* __restrict__ out,
-                                                   uint32_t* __restrict__ status) {
+                                                   uint32_t* __restrict__ status, fast::ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     const DevSym* rows = t.sym;
     const uint16_t* bucket = t.bucket;
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
         head = q * e.mass + (cf - e.cum);  // src/ans.rs:113-114
         out[k] = static_cast<Sym>(s);
     }
-    // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310).
+    // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310).
     for (int pulls = 0; head < kMaxMinHead; ++pulls) {
         if (pulls == 8) { raise_status(status, ANS_E_MISMATCH); return; }
         uint32_t byte = 0;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DevTable t, const uint8_t* __
         else ++generated;
         head = (head << 8) | byte;
     }
-    if (head != kMaxMinHead || src.pos != 0 || generated != 0) raise_status(status, ANS_E_MISMATCH);
+    if (head != ini.head(c) || src.pos != 0 || generated != 0) raise_status(status, ANS_E_MISMATCH);
 }
 
 // Counter-based synthetic iid symbols.
@@ -303,35 +303,6 @@ __global__ __launch_bounds__(256) void k_check_renorm(const uint64_t* __restrict
     out_heads[i] = h;
 }
 
-// TailGenerator::Random (src/ans.rs:129-164): rand_pcg 0.3.1 Pcg64Mcg (MCG-128, XSL-RR-64
-// output) seeded by rand_core 0.6 seed_from_u64 (PCG32 expansion), one byte per draw
-// (rand 0.8.5 Standard<u8> = next_u32() as u8 = next_u64() as u8).  The same restatement as
-// the host's (ans_core.hpp TailGenerator), so GPU samples equal the host's; no reference test
-// pins these bytes (parity unpinned).
-struct Pcg64Mcg {
-    uint64_t lo, hi;
-    __device__ __forceinline__ void seed_from_u64(uint64_t st) {
-        uint32_t w[4];
-        for (int c = 0; c < 4; ++c) {
-            st = st * 6364136223846793005ull + 11634580027462260723ull;
-            const uint32_t xs = static_cast<uint32_t>(((st >> 18) ^ st) >> 27);
-            const uint32_t rot = static_cast<uint32_t>(st >> 59);
-            w[c] = (xs >> rot) | (xs << ((32 - rot) & 31));
-        }
-        lo = (static_cast<uint64_t>(w[1]) << 32 | w[0]) | 3;  // Mcg128Xsl64::new: state | 3
-        hi = static_cast<uint64_t>(w[3]) << 32 | w[2];
-    }
-    __device__ __forceinline__ uint32_t next_byte() {
-        constexpr uint64_t ML = 0x4385DF649FCCF645ull, MH = 0x2360ED051FC65DA4ull;
-        const uint64_t nlo = lo * ML;
-        hi = __umul64hi(lo, ML) + lo * MH + hi * ML;
-        lo = nlo;
-        const uint32_t rot = static_cast<uint32_t>(hi >> 58);
-        const uint64_t xsl = hi ^ lo;
-        return static_cast<uint32_t>((xsl >> rot) | (xsl << ((64 - rot) & 63))) & 0xFFu;
-    }
-};
-
 // Codec::samples (src/ans.rs:42-44) in bulk: chunk c (len = its symbol count) is
 // IID::new(codec, len).pop(&mut Message::random(seed + c)) — decoding from a message whose
 // tail is empty, so every renorm byte is drawn from the generator.
@@ -348,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_iid(DevTable t, uint64_t seed
     }
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (c >= nchunks) return;
-    Pcg64Mcg rng;
+    fast::Pcg64Mcg rng;
     rng.seed_from_u64(seed + c);
     uint64_t head = 1;  // Message::random (src/ans.rs:285-289): head 1, renorm_up(MAX_MIN_HEAD)
     while (head < kMaxMinHead) head = (head << 8) | rng.next_byte();
@@ -458,7 +429,7 @@ uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len, bo
 
 template <typename Sym>
 int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t chunk_len, uint8_t* d_slots,
-                  uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s) {
+                  uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s, fast::ChunkInit ini = {}) {
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
@@ -469,7 +440,7 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         const size_t lds = fast::kEncSharedBytes;  // rows (LDS-row kernels) + ring
         const bool k32 = ft.K < (1ull << 32);
-#define ENC(KM, K32, G, R) fast::k_encode<Sym, KM, K32, G, R><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
+#define ENC(KM, K32, G, R) fast::k_encode<Sym, KM, K32, G, R><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
 #define ENC_KMAX(G, R)                                                         \
         switch (ft.kmax) {                                                     \
         case 1: if (k32) ENC(2, true, G, false); else ENC(2, false, G, false); break; \
@@ -480,7 +451,7 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
                 const size_t wlds = fast::kWideEncCum + 4 * (ft.enc_nl + 1);
-#define ENCW(KM, K32) fast::k_encode_w<Sym, KM, K32><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status)
+#define ENCW(KM, K32) fast::k_encode_w<Sym, KM, K32><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
                 switch (ft.kmax) {
                 case 1: case 2: if (k32) ENCW(2, true); else ENCW(2, false); break;
                 case 3: if (k32) ENCW(3, true); else ENCW(3, false); break;
@@ -507,13 +478,13 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     const unsigned grid = grid_for(nchunks - nfull);
     const size_t lds = gt->lds_bytes ? sizeof(DevSym) * (t.nsym + 1) : 0;
     if (gt->lds_bytes && t.fast)
-        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     else if (gt->lds_bytes)
-        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     else if (t.fast)
-        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     else
-        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, n, chunk_len, nullptr, nfull, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -521,7 +492,7 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
 template <typename Sym>
 int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                   const uint32_t* d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* d_syms,
-                  uint32_t* d_status, hipStream_t s) {
+                  uint32_t* d_status, hipStream_t s, fast::ChunkInit ini = {}) {
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
@@ -539,14 +510,14 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         if (global_table) {
             if constexpr (sizeof(Sym) > 1) {
                 if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0 && slot_cap % 128 == 0)
-                    fast::k_decode_w<Sym><<<grid, fast::kBlock, 160 * 1024, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+                    fast::k_decode_w<Sym><<<grid, fast::kBlock, 160 * 1024, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                 else
-                    fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status);
+                    fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
             }
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
-#define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status)
+#define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
 #define DEC_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true, J4); else DEC(SPP, FAR, false, J4)
 #define DEC_J(SPP, FAR) if (ft.kmax >= 4) { DEC_P(SPP, FAR, true); } else { DEC_P(SPP, FAR, false); }
             if (U * ft.kmax > 60) {  // (kmax = 4)
@@ -564,13 +535,13 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const unsigned grid = grid_for(nchunks - nfull);
     const size_t lds = gt->lds_bytes;
     if (gt->lds_bytes && t.fast)
-        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status, ini);
     else if (gt->lds_bytes)
-        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status, ini);
     else if (t.fast)
-        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status, ini);
     else
-        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, nullptr, nfull, nchunks, gen_kind, out, d_status, ini);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -592,20 +563,21 @@ int launch_gen(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, voi
 // one lane per chunk, slots of slot_cap bytes.
 template <typename Sym>
 int launch_encode_var(ans_gpu_table* gt, const void* d_syms, uint64_t nchunks, const uint64_t* d_starts,
-                      uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s) {
+                      uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s,
+                      fast::ChunkInit ini = {}) {
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     const Sym* syms = static_cast<const Sym*>(d_syms);
     const unsigned grid = grid_for(nchunks);
     const size_t lds = gt->lds_bytes ? sizeof(DevSym) * (t.nsym + 1) : 0;
     if (gt->lds_bytes && t.fast)
-        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     else if (gt->lds_bytes)
-        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     else if (t.fast)
-        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     else
-        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status);
+        k_encode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, syms, 0, 0, d_starts, 0, nchunks, d_slots, slot_cap, d_lens, d_status, ini);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -613,20 +585,20 @@ int launch_encode_var(ans_gpu_table* gt, const void* d_syms, uint64_t nchunks, c
 template <typename Sym>
 int launch_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                       const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind, void* d_syms,
-                      uint32_t* d_status, hipStream_t s) {
+                      uint32_t* d_status, hipStream_t s, fast::ChunkInit ini = {}) {
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     Sym* out = static_cast<Sym*>(d_syms);
     const unsigned grid = grid_for(nchunks);
     const size_t lds = gt->lds_bytes;
     if (gt->lds_bytes && t.fast)
-        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, true><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status, ini);
     else if (gt->lds_bytes)
-        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, true, false><<<grid, kBlock, lds, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status, ini);
     else if (t.fast)
-        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, true><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status, ini);
     else
-        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status);
+        k_decode<Sym, false, false><<<grid, kBlock, 0, s>>>(t, d_in, d_offsets, slot_cap, d_lens, 0, 0, d_starts, 0, nchunks, gen_kind, out, d_status, ini);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
 }
@@ -650,6 +622,7 @@ int launch_sample(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_l
 }
 
 bool valid_width(int w) { return w == 1 || w == 2 || w == 4; }
+bool valid_kind(int k) { return k == ANS_GEN_ZEROS || k == ANS_GEN_EMPTY || k == ANS_GEN_RANDOM; }
 
 int lowest_status(uint32_t bits) {
     for (int k = 1; k < 32; ++k)
@@ -975,7 +948,7 @@ uint64_t pipe_batch_chunks(const ans_gpu* g, uint64_t nchunks, uint64_t chunk_by
 // running offset.  With out == NULL (size query) nothing but the lengths comes back.
 template <typename Sym>
 int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_len, uint8_t* out, uint64_t out_cap,
-                uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+                uint64_t* offsets, uint64_t* lens, uint64_t* total, fast::ChunkInit ini) {
     constexpr uint64_t w = sizeof(Sym);
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     uint64_t slot_cap = 0;
@@ -1001,7 +974,8 @@ int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_
         HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
         HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
         if (s.used) HIP_TRY(hipStreamWaitEvent(sc, s.ev_out, 0));  // dense bytes of batch b - depth copied out
-        int r = launch_encode<Sym>(gt, s.d_syms, nb, chunk_len, s.d_slots, slot_cap, s.d_lens, p->d_status, sc);
+        int r = launch_encode<Sym>(gt, s.d_syms, nb, chunk_len, s.d_slots, slot_cap, s.d_lens, p->d_status, sc,
+                                   fast::ChunkInit{ini.kind, ini.seed + c0});
         if (r) return r;
         k_scan_lens<<<1, 1024, 0, sc>>>(s.d_lens, nc, s.d_offs);
         HIP_TRY(hipGetLastError());
@@ -1060,7 +1034,7 @@ int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_
 // (a container that is not dense); the caller then takes the whole-buffer path.
 template <typename Sym>
 int pipe_decode(ans_gpu_table* gt, const uint8_t* in, const uint64_t* offsets, const uint32_t* l32, uint64_t slot_cap,
-                uint64_t n, uint64_t chunk_len, int gen_kind, void* out) {
+                uint64_t n, uint64_t chunk_len, int gen_kind, void* out, fast::ChunkInit ini) {
     constexpr uint64_t w = sizeof(Sym);
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
@@ -1105,7 +1079,7 @@ int pipe_decode(ans_gpu_table* gt, const uint8_t* in, const uint64_t* offsets, c
                                                               slot_cap);
         HIP_TRY(hipGetLastError());
         if ((rc = launch_decode<Sym>(gt, s.d_slots, nullptr, slot_cap, s.d_lens, nb, chunk_len, gen_kind, s.d_syms,
-                                     p->d_status, sc)))
+                                     p->d_status, sc, fast::ChunkInit{ini.kind, ini.seed + c0})))
             return rc;
         HIP_TRY(hipEventRecord(s.ev_comp, sc));
         HIP_TRY(hipStreamWaitEvent(p->s_out, s.ev_comp, 0));
@@ -1278,7 +1252,7 @@ int pipe_meta(HostPipe* p, uint64_t nchunks) {
 // (k_xfer_out on s_out).  The host only waits at the end.
 template <typename Sym>
 int pipe_encode_mapped(ans_gpu_table* gt, const uint8_t* syms_dev, uint64_t n, uint64_t chunk_len, uint8_t* out_dev,
-                       uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+                       uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total, fast::ChunkInit ini) {
     constexpr uint64_t w = sizeof(Sym);
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     uint64_t slot_cap = 0;
@@ -1305,7 +1279,8 @@ int pipe_encode_mapped(ans_gpu_table* gt, const uint8_t* syms_dev, uint64_t n, u
         HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
         HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
         if (s.used) HIP_TRY(hipStreamWaitEvent(sc, s.ev_out, 0));  // dense bytes of batch b - depth copied out
-        if ((rc = launch_encode<Sym>(gt, s.d_syms, nb, chunk_len, s.d_slots, slot_cap, s.d_lens, p->d_status, sc)))
+        if ((rc = launch_encode<Sym>(gt, s.d_syms, nb, chunk_len, s.d_slots, slot_cap, s.d_lens, p->d_status, sc,
+                                     fast::ChunkInit{ini.kind, ini.seed + c0})))
             return rc;
         if (b > 0) HIP_TRY(hipStreamWaitEvent(sc, p->ev_scan, 0));  // the carry runs in batch order
         k_scan_carry<<<1, 1024, 0, sc>>>(s.d_lens, nc, s.d_offs, p->d_acc, h_offs + c0, h_lens + c0);
@@ -1346,7 +1321,8 @@ int pipe_encode_mapped(ans_gpu_table* gt, const uint8_t* syms_dev, uint64_t n, u
 // decode (compute stream b & 1) -> symbols out (k_xfer on s_out).  No host waits in the loop.
 template <typename Sym>
 int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t* offsets, const uint32_t* l32,
-                       uint64_t slot_cap, uint64_t n, uint64_t chunk_len, int gen_kind, uint8_t* out_dev) {
+                       uint64_t slot_cap, uint64_t n, uint64_t chunk_len, int gen_kind, uint8_t* out_dev,
+                       fast::ChunkInit ini) {
     constexpr uint64_t w = sizeof(Sym);
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
@@ -1390,7 +1366,7 @@ int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t*
                                                               s.d_lens, s.d_slots, slot_cap);
         HIP_TRY(hipGetLastError());
         if ((rc = launch_decode<Sym>(gt, s.d_slots, nullptr, slot_cap, s.d_lens, nb, chunk_len, gen_kind, s.d_syms,
-                                     p->d_status, sc)))
+                                     p->d_status, sc, fast::ChunkInit{ini.kind, ini.seed + c0})))
             return rc;
         HIP_TRY(hipEventRecord(s.ev_comp, sc));
         HIP_TRY(hipStreamWaitEvent(p->s_out, s.ev_comp, 0));
@@ -1412,7 +1388,7 @@ int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t*
 // ans_gpu_encode_var_chunks, also used by the graph dataset coder (ans_graph.hip).
 int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                                const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
-                               uint64_t* lens, uint64_t* total) {
+                               uint64_t* lens, uint64_t* total, int gen_kind, uint64_t seed) {
     if (out && nchunks && (!offsets || !lens)) return ANS_E_ARG;
     *total = 0;
     if (nchunks == 0) return ANS_OK;
@@ -1429,9 +1405,9 @@ int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_by
     HIP_TRY(d_status.alloc(4));
     HIP_TRY(hipMemcpyAsync(d_starts.p, starts, 8 * (nchunks + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
-    int rc = ans_dev_encode_var_chunks(gt, d_syms, sym_bytes, nchunks, static_cast<uint64_t*>(d_starts.p),
-                                       static_cast<uint8_t*>(d_slots.p), slot_cap, static_cast<uint32_t*>(d_lens.p),
-                                       static_cast<uint32_t*>(d_status.p), s);
+    int rc = ans_dev_encode_var_chunks_ex(gt, d_syms, sym_bytes, nchunks, static_cast<uint64_t*>(d_starts.p), gen_kind,
+                                          seed, static_cast<uint8_t*>(d_slots.p), slot_cap,
+                                          static_cast<uint32_t*>(d_lens.p), static_cast<uint32_t*>(d_status.p), s);
     if (rc) return rc;
     int st = 0;
     if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
@@ -1605,36 +1581,53 @@ int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t*
     return ANS_OK;
 }
 
-int ans_dev_encode_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
-                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+int ans_dev_encode_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                             int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
+                             uint32_t* d_status, void* stream) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0 || (slot_cap & 15)) return ANS_E_ARG;
+    if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0 || (slot_cap & 15) || !valid_kind(gen_kind))
+        return ANS_E_ARG;
     if (n && (!d_syms || !d_slots || !d_lens)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
+    const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
-    case 1: return launch_encode<uint8_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s);
-    case 2: return launch_encode<uint16_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s);
-    default: return launch_encode<uint32_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s);
+    case 1: return launch_encode<uint8_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s, ini);
+    case 2: return launch_encode<uint16_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s, ini);
+    default: return launch_encode<uint32_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s, ini);
+    }
+}
+
+int ans_dev_encode_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+    return ans_dev_encode_chunks_ex(gt, d_syms, sym_bytes, n, chunk_len, ANS_GEN_ZEROS, 0, d_slots, slot_cap, d_lens,
+                                    d_status, stream);
+}
+
+int ans_dev_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                             const uint32_t* d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
+                             void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0 || !valid_kind(gen_kind)) return ANS_E_ARG;
+    if (n && (!d_in || !d_lens || !d_syms)) return ANS_E_ARG;
+    if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
+    if (sym_bytes == 2 && gt->t.nsym > 65536) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = pick(gt, stream);
+    const fast::ChunkInit ini{gen_kind, seed};
+    switch (sym_bytes) {
+    case 1: return launch_decode<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s, ini);
+    case 2: return launch_decode<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s, ini);
+    default: return launch_decode<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s, ini);
     }
 }
 
 int ans_dev_decode_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                           const uint32_t* d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* d_syms,
                           int sym_bytes, uint32_t* d_status, void* stream) {
-    (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0) return ANS_E_ARG;
-    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;
-    if (n && (!d_in || !d_lens || !d_syms)) return ANS_E_ARG;
-    if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
-    if (sym_bytes == 2 && gt->t.nsym > 65536) return ANS_E_ARG;
-    HIP_TRY(hipSetDevice(gt->g->device));
-    const hipStream_t s = pick(gt, stream);
-    switch (sym_bytes) {
-    case 1: return launch_decode<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s);
-    case 2: return launch_decode<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s);
-    default: return launch_decode<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s);
-    }
+    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
+    return ans_dev_decode_chunks_ex(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, 0, d_syms, sym_bytes,
+                                    d_status, stream);
 }
 
 int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, void* d_syms, int sym_bytes,
@@ -1691,43 +1684,59 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
     return ANS_OK;
 }
 
-int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
-                              const uint64_t* d_starts, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
-                              uint32_t* d_status, void* stream) {
+int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                                 const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots,
+                                 uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !d_status || !valid_width(sym_bytes) || (slot_cap & 15)) return ANS_E_ARG;
+    if (!gt || !d_status || !valid_width(sym_bytes) || (slot_cap & 15) || !valid_kind(gen_kind)) return ANS_E_ARG;
     if (nchunks && (!d_syms || !d_starts || !d_slots || !d_lens)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
+    const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
-    case 1: return launch_encode_var<uint8_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s);
-    case 2: return launch_encode_var<uint16_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s);
-    default: return launch_encode_var<uint32_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s);
+    case 1: return launch_encode_var<uint8_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
+    case 2: return launch_encode_var<uint16_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
+    default: return launch_encode_var<uint32_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
+    }
+}
+
+int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                              const uint64_t* d_starts, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
+                              uint32_t* d_status, void* stream) {
+    return ans_dev_encode_var_chunks_ex(gt, d_syms, sym_bytes, nchunks, d_starts, ANS_GEN_ZEROS, 0, d_slots, slot_cap,
+                                        d_lens, d_status, stream);
+}
+
+int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                                 const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
+                                 uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();  // drop a stale error another caller left on this thread
+    if (!gt || !d_status || !valid_width(sym_bytes) || !valid_kind(gen_kind)) return ANS_E_ARG;
+    if (nchunks && (!d_in || !d_lens || !d_starts || !d_syms)) return ANS_E_ARG;
+    if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    const hipStream_t s = pick(gt, stream);
+    const fast::ChunkInit ini{gen_kind, seed};
+    switch (sym_bytes) {
+    case 1: return launch_decode_var<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
+    case 2: return launch_decode_var<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
+    default: return launch_decode_var<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
     }
 }
 
 int ans_dev_decode_var_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                               const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
                               void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
-    (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !d_status || !valid_width(sym_bytes)) return ANS_E_ARG;
-    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;
-    if (nchunks && (!d_in || !d_lens || !d_starts || !d_syms)) return ANS_E_ARG;
-    if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
-    HIP_TRY(hipSetDevice(gt->g->device));
-    const hipStream_t s = pick(gt, stream);
-    switch (sym_bytes) {
-    case 1: return launch_decode_var<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s);
-    case 2: return launch_decode_var<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s);
-    default: return launch_decode_var<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s);
-    }
+    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
+    return ans_dev_decode_var_chunks_ex(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, 0, d_syms,
+                                        sym_bytes, d_status, stream);
 }
 
-int ans_gpu_encode_var_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t nchunks,
-                              const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
-                              uint64_t* lens, uint64_t* total) {
+int ans_gpu_encode_var_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t nchunks,
+                                 const uint64_t* starts, int gen_kind, uint64_t seed, uint8_t* out, uint64_t out_cap,
+                                 uint64_t* offsets, uint64_t* lens, uint64_t* total) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !valid_width(sym_bytes) || !total || (nchunks && !starts)) return ANS_E_ARG;
+    if (!gt || !valid_width(sym_bytes) || !total || (nchunks && !starts) || !valid_kind(gen_kind)) return ANS_E_ARG;
     *total = 0;
     if (nchunks == 0) return ANS_OK;
     for (uint64_t c = 0; c < nchunks; ++c)
@@ -1738,14 +1747,23 @@ int ans_gpu_encode_var_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes
     DevBuf d_syms;
     HIP_TRY(d_syms.alloc(n * sym_bytes));
     if (n) HIP_TRY(hipMemcpyAsync(d_syms.p, syms, n * sym_bytes, hipMemcpyHostToDevice, gt->g->stream));
-    return ans_encode_var_from_device(gt, d_syms.p, sym_bytes, nchunks, starts, out, out_cap, offsets, lens, total);
+    return ans_encode_var_from_device(gt, d_syms.p, sym_bytes, nchunks, starts, out, out_cap, offsets, lens, total,
+                                      gen_kind, seed);
 }
 
-int ans_gpu_decode_var_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
-                              const uint64_t* lens, uint64_t nchunks, const uint64_t* starts, int gen_kind, void* out,
-                              int sym_bytes) {
+int ans_gpu_encode_var_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t nchunks,
+                              const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
+                              uint64_t* lens, uint64_t* total) {
+    return ans_gpu_encode_var_chunks_ex(gt, syms, sym_bytes, nchunks, starts, ANS_GEN_ZEROS, 0, out, out_cap, offsets,
+                                        lens, total);
+}
+
+int ans_gpu_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                                 const uint64_t* lens, uint64_t nchunks, const uint64_t* starts, int gen_kind,
+                                 uint64_t seed, void* out, int sym_bytes) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !valid_width(sym_bytes) || (nchunks && (!starts || !offsets || !lens))) return ANS_E_ARG;
+    if (!gt || !valid_width(sym_bytes) || (nchunks && (!starts || !offsets || !lens)) || !valid_kind(gen_kind))
+        return ANS_E_ARG;
     if (nchunks == 0) return ANS_OK;
     std::vector<uint32_t> l32(nchunks);
     for (uint64_t c = 0; c < nchunks; ++c) {
@@ -1769,15 +1787,23 @@ int ans_gpu_decode_var_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_
     HIP_TRY(hipMemcpyAsync(d_lens.p, l32.data(), 4 * nchunks, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d_starts.p, starts, 8 * (nchunks + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
-    int rc = ans_dev_decode_var_chunks(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_offs.p), 0,
-                                       static_cast<uint32_t*>(d_lens.p), nchunks, static_cast<uint64_t*>(d_starts.p),
-                                       gen_kind, d_out.p, sym_bytes, static_cast<uint32_t*>(d_status.p), s);
+    int rc = ans_dev_decode_var_chunks_ex(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_offs.p), 0,
+                                          static_cast<uint32_t*>(d_lens.p), nchunks,
+                                          static_cast<uint64_t*>(d_starts.p), gen_kind, seed, d_out.p, sym_bytes,
+                                          static_cast<uint32_t*>(d_status.p), s);
     if (rc) return rc;
     int st = 0;
     if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
     if (st) return st;
     if (n) HIP_TRY(hipMemcpy(out, d_out.p, n * sym_bytes, hipMemcpyDeviceToHost));
     return ANS_OK;
+}
+
+int ans_gpu_decode_var_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                              const uint64_t* lens, uint64_t nchunks, const uint64_t* starts, int gen_kind, void* out,
+                              int sym_bytes) {
+    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
+    return ans_gpu_decode_var_chunks_ex(gt, in, in_len, offsets, lens, nchunks, starts, gen_kind, 0, out, sym_bytes);
 }
 
 int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const uint32_t* d_lens,
@@ -1816,10 +1842,12 @@ int ans_dev_status(ans_gpu* g, const uint32_t* d_status, void* stream, int* stat
     return ANS_OK;
 }
 
-int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
-                          uint8_t* out, uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+int ans_gpu_encode_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                             int gen_kind, uint64_t seed, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
+                             uint64_t* lens, uint64_t* total) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
-    if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || !total) return ANS_E_ARG;
+    if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || !total || !valid_kind(gen_kind)) return ANS_E_ARG;
+    const fast::ChunkInit ini{gen_kind, seed};
     if (n && !syms) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (out && nchunks && (!offsets || !lens)) return ANS_E_ARG;
@@ -1831,26 +1859,33 @@ int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, ui
     uint8_t* out_dev = out && syms_dev ? mapped_ptr(out) : nullptr;
     if (syms_dev && (!out || out_dev)) {
         switch (sym_bytes) {
-        case 1: return pipe_encode_mapped<uint8_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total);
-        case 2: return pipe_encode_mapped<uint16_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total);
-        default: return pipe_encode_mapped<uint32_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total);
+        case 1: return pipe_encode_mapped<uint8_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total, ini);
+        case 2: return pipe_encode_mapped<uint16_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total, ini);
+        default: return pipe_encode_mapped<uint32_t>(gt, syms_dev, n, chunk_len, out_dev, out_cap, offsets, lens, total, ini);
         }
     }
     switch (sym_bytes) {
-    case 1: return pipe_encode<uint8_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total);
-    case 2: return pipe_encode<uint16_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total);
-    default: return pipe_encode<uint32_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total);
+    case 1: return pipe_encode<uint8_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total, ini);
+    case 2: return pipe_encode<uint16_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total, ini);
+    default: return pipe_encode<uint32_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total, ini);
     }
 }
 
-int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
-                          const uint64_t* lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* out,
-                          int sym_bytes) {
+int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                          uint8_t* out, uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+    return ans_gpu_encode_chunks_ex(gt, syms, sym_bytes, n, chunk_len, ANS_GEN_ZEROS, 0, out, out_cap, offsets, lens,
+                                    total);
+}
+
+int ans_gpu_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                             const uint64_t* lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
+                             void* out, int sym_bytes) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks && (!in || !offsets || !lens || !out)) return ANS_E_ARG;
-    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;
+    if (!valid_kind(gen_kind)) return ANS_E_ARG;
+    const fast::ChunkInit ini{gen_kind, seed};
     if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
     std::vector<uint32_t> l32(nchunks);
     for (uint64_t j = 0; j < nchunks; ++j) {
@@ -1871,16 +1906,16 @@ int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len,
         uint8_t* out_dev = in_dev ? mapped_ptr(out) : nullptr;
         if (in_dev && out_dev) {
             switch (sym_bytes) {
-            case 1: rc = pipe_decode_mapped<uint8_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev); break;
-            case 2: rc = pipe_decode_mapped<uint16_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev); break;
-            default: rc = pipe_decode_mapped<uint32_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev); break;
+            case 1: rc = pipe_decode_mapped<uint8_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev, ini); break;
+            case 2: rc = pipe_decode_mapped<uint16_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev, ini); break;
+            default: rc = pipe_decode_mapped<uint32_t>(gt, in_dev, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out_dev, ini); break;
             }
             if (rc != kPipeScattered) return rc;
         }
         switch (sym_bytes) {
-        case 1: rc = pipe_decode<uint8_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out); break;
-        case 2: rc = pipe_decode<uint16_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out); break;
-        default: rc = pipe_decode<uint32_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out); break;
+        case 1: rc = pipe_decode<uint8_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out, ini); break;
+        case 2: rc = pipe_decode<uint16_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out, ini); break;
+        default: rc = pipe_decode<uint32_t>(gt, in, offsets, l32.data(), slot_cap, n, chunk_len, gen_kind, out, ini); break;
         }
         if (rc != kPipeScattered) return rc;
     }
@@ -1903,9 +1938,9 @@ int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len,
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMemsetAsync(d_status.p, 0, sizeof(uint32_t), s));
-    int rc = ans_dev_decode_chunks(gt, static_cast<uint8_t*>(d_slots.p), nullptr, slot_cap,
-                                   static_cast<uint32_t*>(d_lens.p), n, chunk_len, gen_kind, d_out.p, sym_bytes,
-                                   static_cast<uint32_t*>(d_status.p), s);
+    int rc = ans_dev_decode_chunks_ex(gt, static_cast<uint8_t*>(d_slots.p), nullptr, slot_cap,
+                                      static_cast<uint32_t*>(d_lens.p), n, chunk_len, gen_kind, seed, d_out.p,
+                                      sym_bytes, static_cast<uint32_t*>(d_status.p), s);
     if (rc) return rc;
     int st = 0;
     rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st);
@@ -1913,6 +1948,13 @@ int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len,
     if (st) return st;
     if (n) HIP_TRY(hipMemcpy(out, d_out.p, n * sym_bytes, hipMemcpyDeviceToHost));
     return ANS_OK;
+}
+
+int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                          const uint64_t* lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* out,
+                          int sym_bytes) {
+    if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
+    return ans_gpu_decode_chunks_ex(gt, in, in_len, offsets, lens, n, chunk_len, gen_kind, 0, out, sym_bytes);
 }
 
 }  // extern "C"

@@ -61,7 +61,8 @@ __device__ __forceinline__ double rcp_newton(uint32_t p) {
 template <typename Sym, int KMAX, bool kK32>
 __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
                                                          uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
-                                                         uint32_t* __restrict__ lens, uint32_t* __restrict__ status) {
+                                                         uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
+                                                         ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     {
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideEncCum);
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     const uint32_t exp_norm = 0x43300000u * norm;
     const uint32_t* gcum = t.cum;
 
-    uint64_t head = kMaxMinHead;  // Message::zeros()
+    uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
     FunnelT<kWideRing> f{0, 0, 0, ring.col, ring.col};
     uint32_t fp = 0, over = 0;
     uint32_t minmass = ~0u;
@@ -313,7 +314,8 @@ template <typename Sym>
 __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
                                                          uint64_t slot_cap, const uint32_t* __restrict__ lens,
                                                          uint64_t chunk_len, uint64_t nfull, int gen_kind,
-                                                         Sym* __restrict__ out, uint32_t* __restrict__ status) {
+                                                         Sym* __restrict__ out, uint32_t* __restrict__ status,
+                                                         ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
     {  // the prefix tables: bucket s0 values (u16), then cdf(0 .. nlp + 5)
         const uint32_t* gs = reinterpret_cast<const uint32_t*>(t.dec_w_s0);
@@ -436,11 +438,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
         d[2] = q[2];
         d[3] = q[3];
     }
-    // assert_eq!(initial, m) with initial = Message::zeros() (src/ans.rs:56, 302-310)
+    // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
     const int32_t remaining = ch.P + 4;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
-    else if (ch.head != kMaxMinHead || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+    else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
 
 }  // namespace fast

@@ -670,3 +670,70 @@ def test_wide_kernel_errors(gpu):
     with pytest.raises(A.AnsError) as e:
         gt.encode_chunks(bad, 4096)
     assert e.value.code == A.ANS_E_SYMBOL
+
+
+# ---------------------------------------------------------------- Message::random initial messages
+def _roundtrip_random(gpu, masses, syms, chunk_len, dtype, seed):
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    s = np.asarray(syms).astype(dtype)
+    data, offsets, lens = gt.encode_chunks(s, chunk_len, gen_kind=A.GEN_RANDOM, seed=seed)
+    od, oo, ol = orc.encode_chunks(masses, np.asarray(syms, np.uint32), chunk_len, kind=orc.RANDOM, seed=seed)
+    assert np.array_equal(lens, ol)
+    assert data.tobytes() == od.tobytes()
+    back = gt.decode_chunks(data, offsets, lens, len(s), chunk_len, dtype, gen_kind=A.GEN_RANDOM, seed=seed)
+    assert np.array_equal(back, s)
+    with pytest.raises(A.AnsError) as e:  # another seed's initial message is not where decoding ends
+        gt.decode_chunks(data, offsets, lens, len(s), chunk_len, dtype, gen_kind=A.GEN_RANDOM, seed=seed + 1)
+    assert e.value.code == A.ANS_E_MISMATCH
+    return data
+
+
+@pytest.mark.parametrize("size,chunks", [(1000, 1), (100000, 1), (100000, 64)])
+def test_random_message_multiset_fixtures(gpu, size, chunks, multiset_masses, multiset_vectors):
+    """The reference harness codes each fixture from Message::random(0) (src/multiset.rs:174,
+    src/benchmark.rs:698-700): one chunk with seed 0 is exactly that message (C1 on the HIP
+    path); 64 chunks give chunk c Message::random(c) (C2 layout)."""
+    syms = multiset_vectors[size]
+    chunk_len = -(-size // chunks)
+    for dtype in (np.uint16, np.uint32):
+        _roundtrip_random(gpu, multiset_masses, syms, chunk_len, dtype, 0)
+
+
+@pytest.mark.parametrize("which", ["c3", "c4", "bernoulli"])
+def test_random_message_fast_kernels(gpu, which):
+    """Message::random(seed + c) on the fast kernels (LDS rows / wide tables), against the oracle."""
+    if which == "c3":
+        masses, n, dtype = A.c3_masses(), 1100 * 4096 + 5, np.uint8
+    elif which == "c4":
+        masses, n, dtype = A.c4_masses(), 600 * 4096, np.uint16
+    else:
+        masses, n, dtype = np.array([(1 << 28) - 26843, 26843], np.uint64), 700 * 4096, np.uint8
+    syms = orc.gen_iid(masses, 9, 0, n)
+    _roundtrip_random(gpu, masses, syms, 4096, dtype, 12345)
+
+
+def test_random_message_device_api(gpu):
+    """ans_dev_*_chunks_ex: slot layout, device buffers, seed offsets per chunk."""
+    torch = pytest.importorskip("torch")
+    masses = A.c3_masses()
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    n, L, seed = 1 << 22, 4096, 777
+    stream = torch.cuda.Stream()
+    syms = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gt.dev_gen_iid(3, 0, n, syms, 1, stream)
+    cap = gt.slot_capacity(L)
+    slots = torch.empty((n // L) * cap, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(n // L, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    gt.dev_encode(syms, 1, n, L, slots, cap, lens, status, stream, gen_kind=A.GEN_RANDOM, seed=seed)
+    out = torch.empty_like(syms)
+    gt.dev_decode(slots, None, cap, lens, n, L, out, 1, status, stream, gen_kind=A.GEN_RANDOM, seed=seed)
+    assert gpu.status(status, stream) == 0
+    assert torch.equal(out, syms)
+    lh = lens.cpu().numpy()
+    ref = orc.gen_iid(masses, 3, 0, n)
+    od, oo, ol = orc.encode_chunks(masses, ref, L, kind=orc.RANDOM, seed=seed)
+    assert np.array_equal(lh.astype(np.uint64), ol)
+    sl = slots.cpu().numpy()
+    for c in (0, 1, 511, 1023):
+        assert sl[c * cap: c * cap + lh[c]].tobytes() == od[int(oo[c]):int(oo[c]) + int(ol[c])].tobytes()

@@ -173,3 +173,28 @@ def test_gen_iid_matches_python_splitmix():
         cf = (r * norm) >> 64
         ref.append(int(np.searchsorted(cums, cf, side="right")) - 1)
     assert orc.gen_iid(masses, 9, 100, 500).tolist() == ref
+
+
+def test_random_initial_message_containers(multiset_masses, multiset_vectors):
+    """Chunks begun as Message::random(seed + c) (the reference harness' initial message,
+    src/multiset.rs:174): the oracle's container equals the host coder's IID push on
+    Message::random, and decoding with the tail's generator state kept (src/ans.rs:57) returns
+    every chunk to its initial message (src/ans.rs:56)."""
+    import ans_amd as A
+    syms = multiset_vectors[10000]
+    cat = A.Categorical(multiset_masses)
+    d, o, ln = orc.encode_chunks(multiset_masses, syms, len(syms), kind=orc.RANDOM, seed=0)
+    m = A.Message.random(0)
+    A.IID(cat, len(syms)).push(m, syms)
+    assert m.flatten() == d.tobytes()  # the reference harness' single message
+    for chunk_len, seed in [(len(syms), 0), (157, 5), (1, 11)]:
+        d, o, ln = orc.encode_chunks(multiset_masses, syms, chunk_len, kind=orc.RANDOM, seed=seed)
+        back = orc.decode_chunks(multiset_masses, d, o, ln, len(syms), chunk_len, kind=orc.RANDOM, seed=seed)
+        assert np.array_equal(back, syms)
+        for c in (0, len(ln) - 1):  # chunk c is the host coder's message from Message::random(seed + c)
+            a, b = c * chunk_len, min(len(syms), (c + 1) * chunk_len)
+            mm = A.Message.random(seed + c)
+            A.IID(cat, b - a).push(mm, syms[a:b])
+            assert mm.flatten() == d[int(o[c]):int(o[c]) + int(ln[c])].tobytes()
+        with pytest.raises(RuntimeError):  # the wrong seed does not return to the initial message
+            orc.decode_chunks(multiset_masses, d, o, ln, len(syms), chunk_len, kind=orc.RANDOM, seed=seed + 1)
