@@ -110,7 +110,8 @@ int ans_pop_iid(ans_msg *m, const ans_table *t, uint32_t *out, size_t n);
  *     Its stream is byte-identical to that.  Decode is IID::pop on
  *     Message::unflatten(stream) (src/codec.rs:422-424, src/ans.rs:107-116,262).
  *     Symbols are unsigned integers of sym_bytes = 1, 2 or 4 bytes.
- *     Supported tables: 1 <= nsym <= 65536 and norm < 2^32 (ANS_E_NORM_RANGE otherwise).
+ *     Tables with 1 <= nsym <= 65536 and norm < 2^32 take the table kernels; larger ones the
+ *     exact 64-bit kernels of section 4b (norm <= 2^56, else ANS_E_NORM_RANGE).
  * ====================================================================== */
 typedef struct ans_gpu ans_gpu;
 typedef struct ans_gpu_table ans_gpu_table;
@@ -244,6 +245,46 @@ int ans_dev_check_renorm(ans_gpu *g, const uint64_t *d_heads, const uint32_t *d_
                          uint64_t *d_out_heads, uint32_t *d_out_k, void *stream);
 /* Synchronises `stream` and maps the device status word to the lowest set status. */
 int ans_dev_status(ans_gpu *g, const uint32_t *d_status, void *stream, int *status);
+
+/* ======================================================================
+ * (4b) The other static codecs of src/codec.rs in bulk (exact 64-bit generic kernels, one lane
+ *      per chunk; chunk c is one reference message from the initial message gen_kind / seed
+ *      gives it, as in the _ex calls of section 4).  sym_bytes may also be 8 here.
+ *      A Categorical with norm >= 2^32 (up to 2^56) or more than 65536 symbols takes these
+ *      kernels through the section-4 calls themselves (ans_gpu_table_create accepts it; its
+ *      paths flags are 0; ans_dev_gen_iid / sample_iid return ANS_E_NORM_RANGE for it).
+ * ====================================================================== */
+/* IID<Uniform(size)>  src/codec.rs:13-49; size <= MAX_SIZE = 2^46 (src/ans.rs:22, ANS_E_NORM_RANGE
+ * beyond).  A symbol >= size is ANS_E_SYMBOL (the reference does not check it and codes garbage). */
+int ans_gpu_uniform_encode_chunks(ans_gpu *g, uint64_t size, const void *syms, int sym_bytes, uint64_t n,
+                                  uint64_t chunk_len, int gen_kind, uint64_t seed, uint8_t *out, uint64_t out_cap,
+                                  uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_uniform_decode_chunks(ans_gpu *g, uint64_t size, const uint8_t *in, uint64_t in_len,
+                                  const uint64_t *offsets, const uint64_t *lens, uint64_t n, uint64_t chunk_len,
+                                  int gen_kind, uint64_t seed, void *out, int sym_bytes);
+/* IID<LogUniform::new(excl_max_bits)>  src/codec.rs:561-611 (excl_max_bits <= 64): per symbol a
+ * Uniform(2^(bits-1)) push of its low bits, then Uniform(excl_max_bits + 1) of bits = 64 - clz(x);
+ * MaxBenfordIID's item (src/param_codec.rs:117-119).  bits > excl_max_bits is ANS_E_SYMBOL,
+ * x >= 2^47 is ANS_E_NORM_RANGE (Uniform::new's assert).  A chunk whose pushes would draw from
+ * the tail generator (the tail's num_generated, which no byte container carries) is
+ * ANS_E_MISMATCH. */
+int ans_gpu_loguniform_encode_chunks(ans_gpu *g, uint32_t excl_max_bits, const void *syms, int sym_bytes, uint64_t n,
+                                     uint64_t chunk_len, int gen_kind, uint64_t seed, uint8_t *out, uint64_t out_cap,
+                                     uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_loguniform_decode_chunks(ans_gpu *g, uint32_t excl_max_bits, const uint8_t *in, uint64_t in_len,
+                                     const uint64_t *offsets, const uint64_t *lens, uint64_t n, uint64_t chunk_len,
+                                     int gen_kind, uint64_t seed, void *out, int sym_bytes);
+/* Independent<Categorical>  src/codec.rs:366-403: position k codes with table table_ids[k] of the set
+ * (the Categoricals uploaded once; norms up to 2^56).  Chunk c = positions [c*chunk_len, ...). */
+typedef struct ans_gpu_tableset ans_gpu_tableset;
+int ans_gpu_tableset_create(ans_gpu *g, const ans_table *const *tables, uint32_t ntables, ans_gpu_tableset **out);
+void ans_gpu_tableset_free(ans_gpu_tableset *ts);
+int ans_gpu_independent_encode_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const void *syms, int sym_bytes,
+                                      uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed, uint8_t *out,
+                                      uint64_t out_cap, uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_independent_decode_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const uint8_t *in,
+                                      uint64_t in_len, const uint64_t *offsets, const uint64_t *lens, uint64_t n,
+                                      uint64_t chunk_len, int gen_kind, uint64_t seed, void *out, int sym_bytes);
 
 /* ======================================================================
  * (5) Graph models' bulk-IID caller — DenseSetIID<EdgeIndex, AllEdgeIndices> with an

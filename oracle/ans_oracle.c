@@ -480,3 +480,138 @@ int orc_gen_iid(const uint64_t *masses, uint32_t nsym, uint64_t seed, uint64_t s
     orc_cat_free(c);
     return ORC_OK;
 }
+
+/* ---------------- the other static codecs in chunks (GPU section 4b) ----------------
+ * Chunk j covers symbols [j*L, min(n, (j+1)*L)) and is one message from the initial message of
+ * `kind` (seed + j for RANDOM), pushed in reverse (IID/Independent, codec.rs:388-391,415-420). */
+enum { ORC_CODEC_UNIFORM = 0, ORC_CODEC_LOGUNIFORM = 1, ORC_CODEC_INDEPENDENT = 2 };
+
+typedef struct {
+    int codec;
+    uint64_t param;          /* Uniform: size; LogUniform: excl_max_bits */
+    orc_cat **tables;        /* Independent */
+    const uint32_t *tids;
+} codec_t;
+
+/* LogUniform (codec.rs:568-586): get_bits = 64 - leading_zeros */
+static uint64_t get_bits(uint64_t x) { return x ? 64u - (uint64_t)__builtin_clzll(x) : 0u; }
+
+static int codec_push(orc_msg *m, const codec_t *c, uint64_t x, uint64_t k) {
+    switch (c->codec) {
+    case ORC_CODEC_UNIFORM:
+        if (c->param > (1ull << 46)) return ORC_E_NORM_RANGE; /* Uniform::new (codec.rs:34-37) */
+        return orc_uniform_push(m, c->param, x);
+    case ORC_CODEC_LOGUNIFORM: {
+        uint64_t nbits = c->param + 1, bits = get_bits(x);
+        if (bits >= nbits) return ORC_E_SYMBOL; /* assert!(bits < self.bits.size) */
+        if (bits != 0) {
+            uint64_t size = 1ull << (bits - 1);
+            if (size > (1ull << 46)) return ORC_E_NORM_RANGE;
+            int e = orc_uniform_push(m, size, x & ~size);
+            if (e) return e;
+        }
+        return orc_uniform_push(m, nbits, bits);
+    }
+    default:
+        return orc_cat_push(m, c->tables[c->tids[k]], x);
+    }
+}
+
+static int codec_pop(orc_msg *m, const codec_t *c, uint64_t k, uint64_t *x) {
+    switch (c->codec) {
+    case ORC_CODEC_UNIFORM:
+        return orc_uniform_pop(m, c->param, x);
+    case ORC_CODEC_LOGUNIFORM: {
+        uint64_t bits = 0, low = 0;
+        int e = orc_uniform_pop(m, c->param + 1, &bits);
+        if (e) return e;
+        if (bits == 0) { *x = 0; return ORC_OK; }
+        uint64_t size = 1ull << (bits - 1);
+        e = orc_uniform_pop(m, size, &low);
+        *x = low | size;
+        return e;
+    }
+    default:
+        return orc_cat_pop(m, c->tables[c->tids[k]], x);
+    }
+}
+
+static codec_t codec_make(int codec, uint64_t param, uint32_t ntables, const uint64_t *masses, const uint32_t *nsyms,
+                          const uint32_t *tids) {
+    codec_t c = {codec, param, NULL, tids};
+    if (codec == ORC_CODEC_INDEPENDENT) {
+        c.tables = (orc_cat **)calloc(ntables ? ntables : 1, sizeof(orc_cat *));
+        for (uint32_t t = 0; t < ntables; ++t) {
+            c.tables[t] = orc_cat_new(masses, nsyms[t]);
+            masses += nsyms[t];
+        }
+    }
+    return c;
+}
+
+static void codec_free(codec_t *c, uint32_t ntables) {
+    if (!c->tables) return;
+    for (uint32_t t = 0; t < ntables; ++t) orc_cat_free(c->tables[t]);
+    free(c->tables);
+}
+
+int orc_codec_encode_chunks(int codec, uint64_t param, uint32_t ntables, const uint64_t *masses, const uint32_t *nsyms,
+                            const uint32_t *tids, const uint64_t *syms, uint64_t n, uint64_t chunk_len, int kind,
+                            uint64_t seed, uint8_t *out, uint64_t out_cap, uint64_t *offsets, uint64_t *lens) {
+    if (chunk_len == 0) return ORC_E_LEN;
+    codec_t c = codec_make(codec, param, ntables, masses, nsyms, tids);
+    uint64_t nchunks = (n + chunk_len - 1) / chunk_len, pos = 0;
+    int rc = ORC_OK;
+    for (uint64_t j = 0; j < nchunks && rc == ORC_OK; ++j) {
+        uint64_t a = j * chunk_len, b = a + chunk_len < n ? a + chunk_len : n;
+        orc_msg *m = orc_msg_new(kind, seed + j);
+        for (uint64_t k = b; k-- > a && rc == ORC_OK;) rc = codec_push(m, &c, syms[k], k);
+        if (rc == ORC_OK) {
+            uint64_t len = orc_msg_flatten(m, NULL, 0);
+            if (pos + len > out_cap) rc = ORC_E_LEN;
+            else {
+                orc_msg_flatten(m, out + pos, len);
+                offsets[j] = pos;
+                lens[j] = len;
+                pos += len;
+            }
+        }
+        orc_msg_free(m);
+    }
+    codec_free(&c, ntables);
+    return rc;
+}
+
+/* Decodes every chunk and checks that it returns to its initial message (ans.rs:56); for RANDOM
+ * the tail keeps the encoder's generator state (Message::unflatten(m.flatten()), ans.rs:57). */
+int orc_codec_decode_chunks(int codec, uint64_t param, uint32_t ntables, const uint64_t *masses, const uint32_t *nsyms,
+                            const uint32_t *tids, const uint8_t *in, const uint64_t *offsets, const uint64_t *lens,
+                            uint64_t n, uint64_t chunk_len, int kind, uint64_t seed, uint64_t *out) {
+    if (chunk_len == 0) return ORC_E_LEN;
+    codec_t c = codec_make(codec, param, ntables, masses, nsyms, tids);
+    uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    int rc = ORC_OK;
+    for (uint64_t j = 0; j < nchunks && rc == ORC_OK; ++j) {
+        uint64_t a = j * chunk_len, b = a + chunk_len < n ? a + chunk_len : n;
+        orc_msg *m;
+        if (kind == GEN_RANDOM) {
+            m = orc_msg_new(kind, seed + j);
+            if (m && tail_reserve(&m->tail, lens[j] ? lens[j] : 1) == 0) {
+                if (lens[j]) memcpy(m->tail.el, in + offsets[j], lens[j]);
+                m->tail.len = lens[j];
+                m->head = 0;
+            }
+        } else {
+            m = orc_msg_unflatten(in + offsets[j], lens[j], kind, seed + j);
+        }
+        for (uint64_t k = a; k < b && rc == ORC_OK; ++k) rc = codec_pop(m, &c, k, &out[k]);
+        if (rc == ORC_OK) {
+            orc_msg *init = orc_msg_new(kind, seed + j);
+            if (!orc_msg_equal(init, m)) rc = ORC_E_LEN;
+            orc_msg_free(init);
+        }
+        orc_msg_free(m);
+    }
+    codec_free(&c, ntables);
+    return rc;
+}

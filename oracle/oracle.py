@@ -58,6 +58,10 @@ def lib():
             "orc_decode_chunks": (ctypes.c_int, [vp, u32, vp, vp, vp, u64, u64, ctypes.c_int, u64, vp]),
             "orc_gen_iid": (ctypes.c_int, [vp, u32, u64, u64, u64, vp]),
             "orc_splitmix64": (u64, [u64]),
+            "orc_codec_encode_chunks": (ctypes.c_int, [ctypes.c_int, u64, u32, vp, vp, vp, vp, u64, u64, ctypes.c_int,
+                                                       u64, vp, u64, vp, vp]),
+            "orc_codec_decode_chunks": (ctypes.c_int, [ctypes.c_int, u64, u32, vp, vp, vp, vp, vp, vp, u64, u64,
+                                                       ctypes.c_int, u64, vp]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -265,3 +269,52 @@ def dense_set(edges, num_nodes, directed, loops):
     d = np.zeros(n, np.uint8)
     d[s] = 1
     return d
+
+
+# ---- the other static codecs in chunks (the GPU's section 4b): Uniform, LogUniform, Independent
+CODEC_UNIFORM, CODEC_LOGUNIFORM, CODEC_INDEPENDENT = 0, 1, 2
+
+
+def _codec_args(codec, param, tables, tids):
+    if codec != CODEC_INDEPENDENT:
+        return codec, param, 0, None, None, None, []
+    ms = [np.asarray(t, dtype=np.uint64) for t in tables]
+    masses = np.ascontiguousarray(np.concatenate(ms))
+    nsyms = np.ascontiguousarray(np.array([len(t) for t in ms], np.uint32))
+    tids = np.ascontiguousarray(np.asarray(tids, dtype=np.uint32))
+    return codec, param, len(ms), _ptr(masses), _ptr(nsyms), _ptr(tids), [masses, nsyms, tids]
+
+
+def codec_encode_chunks(codec, syms, chunk_len, param=0, tables=None, tids=None, kind=ZEROS, seed=0):
+    """Returns (dense bytes, offsets, lens) of IID<Uniform(param)>, IID<LogUniform(param)> or
+    Independent<Categorical>(tables, per-position tids), one message per chunk."""
+    syms = np.ascontiguousarray(np.asarray(syms, dtype=np.uint64))
+    n = len(syms)
+    nchunks = (n + chunk_len - 1) // chunk_len
+    cap = 16 * n + 16 * nchunks + 16
+    out = np.zeros(cap, np.uint8)
+    offsets = np.zeros(max(nchunks, 1), np.uint64)
+    lens = np.zeros(max(nchunks, 1), np.uint64)
+    c, p, nt, mp, np_, tp, keep = _codec_args(codec, param, tables, tids)
+    rc = lib().orc_codec_encode_chunks(c, p, nt, mp, np_, tp, _ptr(syms), n, chunk_len, kind, seed, _ptr(out), cap,
+                                       _ptr(offsets), _ptr(lens))
+    if rc:
+        raise RuntimeError(f"oracle codec encode failed rc={rc}")
+    total = int(lens[:nchunks].sum())
+    return out[:total].copy(), offsets[:nchunks].copy(), lens[:nchunks].copy()
+
+
+def codec_decode_chunks(codec, data, offsets, lens, n, chunk_len, param=0, tables=None, tids=None, kind=ZEROS, seed=0):
+    data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+    if data.size == 0:
+        data = np.zeros(1, np.uint8)
+    offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+    lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    out = np.zeros(max(n, 1), np.uint64)
+    c, p, nt, mp, np_, tp, keep = _codec_args(codec, param, tables, tids)
+    rc = lib().orc_codec_decode_chunks(c, p, nt, mp, np_, tp, _ptr(data), _ptr(offsets), _ptr(lens), n, chunk_len,
+                                       kind, seed, _ptr(out))
+    if rc:
+        raise RuntimeError(f"oracle codec decode failed rc={rc}")
+    return out[:n]
+

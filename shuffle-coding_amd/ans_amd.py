@@ -85,6 +85,14 @@ SIGNATURES = {
     "ans_gpu_decode_var_chunks_ex": (ci, [vp, vp, u64, vp, vp, u64, vp, ci, u64, vp, ci]),
     "ans_dev_encode_var_chunks_ex": (ci, [vp, vp, ci, u64, vp, ci, u64, vp, u64, vp, vp, vp]),
     "ans_dev_decode_var_chunks_ex": (ci, [vp, vp, vp, u64, vp, u64, vp, ci, u64, vp, ci, vp, vp]),
+    "ans_gpu_uniform_encode_chunks": (ci, [vp, u64, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_uniform_decode_chunks": (ci, [vp, u64, vp, u64, vp, vp, u64, u64, ci, u64, vp, ci]),
+    "ans_gpu_loguniform_encode_chunks": (ci, [vp, ctypes.c_uint32, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_loguniform_decode_chunks": (ci, [vp, ctypes.c_uint32, vp, u64, vp, vp, u64, u64, ci, u64, vp, ci]),
+    "ans_gpu_tableset_create": (ci, [vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.POINTER(vp)]),
+    "ans_gpu_tableset_free": (None, [vp]),
+    "ans_gpu_independent_encode_chunks": (ci, [vp, vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_independent_decode_chunks": (ci, [vp, vp, vp, u64, vp, vp, u64, u64, ci, u64, vp, ci]),
     "ans_gpu_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_decode_chunks": (ci, [vp, vp, u64, vp, vp, u64, u64, ci, vp, ci]),
     "ans_dev_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, vp]),
@@ -612,7 +620,7 @@ def _sptr(stream):
     return stream.cuda_stream
 
 
-_WIDTH = {np.dtype(np.uint8): 1, np.dtype(np.uint16): 2, np.dtype(np.uint32): 4}
+_WIDTH = {np.dtype(np.uint8): 1, np.dtype(np.uint16): 2, np.dtype(np.uint32): 4, np.dtype(np.uint64): 8}
 
 
 class GpuTable:
@@ -737,6 +745,117 @@ class GpuTable:
     def dev_gen_iid(self, seed, start, n, d_syms, sym_bytes, stream=None):
         _check(lib().ans_dev_gen_iid(self.h, seed, start, n, _dptr(d_syms), sym_bytes, _sptr(stream)),
                "ans_dev_gen_iid")
+
+
+# ============================================================== other static codecs (section 4b)
+def _enc_buffers(n, chunk_len, per_symbol=8):
+    nchunks = -(-n // chunk_len)
+    out = np.empty(max(per_symbol * n + 16 * nchunks + 64, 1), np.uint8)
+    return nchunks, out, np.zeros(max(nchunks, 1), np.uint64), np.zeros(max(nchunks, 1), np.uint64)
+
+
+def _dec_arrays(data, offsets, lens):
+    data = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+    return (data, np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64)),
+            np.ascontiguousarray(np.asarray(lens, dtype=np.uint64)))
+
+
+class GpuUniform:
+    """IID<Uniform(size)> in chunks on the GPU (src/codec.rs:13-49; size <= 2^46)."""
+
+    def __init__(self, gpu, size):
+        self.gpu, self.size = gpu, int(size)
+
+    def encode_chunks(self, syms, chunk_len, gen_kind=GEN_ZEROS, seed=0):
+        syms = np.ascontiguousarray(syms)
+        n = len(syms)
+        nchunks, out, offsets, lens = _enc_buffers(n, chunk_len)
+        total = u64(0)
+        _check(lib().ans_gpu_uniform_encode_chunks(self.gpu.h, self.size, _np_ptr(syms), _WIDTH[syms.dtype], n,
+                                                   chunk_len, gen_kind, seed, _np_ptr(out), len(out), _np_ptr(offsets),
+                                                   _np_ptr(lens), ctypes.byref(total)), "ans_gpu_uniform_encode_chunks")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode_chunks(self, data, offsets, lens, n, chunk_len, dtype=np.uint64, gen_kind=GEN_ZEROS, seed=0):
+        data, offsets, lens = _dec_arrays(data, offsets, lens)
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_uniform_decode_chunks(self.gpu.h, self.size, _np_ptr(data) if data.size else None,
+                                                   data.size, _np_ptr(offsets), _np_ptr(lens), n, chunk_len, gen_kind,
+                                                   seed, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
+               "ans_gpu_uniform_decode_chunks")
+        return out[:n]
+
+
+class GpuLogUniform:
+    """IID<LogUniform::new(excl_max_bits)> in chunks on the GPU (src/codec.rs:561-611), the item
+    of MaxBenfordIID (src/param_codec.rs:117-119)."""
+
+    def __init__(self, gpu, excl_max_bits):
+        self.gpu, self.excl_max_bits = gpu, int(excl_max_bits)
+
+    def encode_chunks(self, syms, chunk_len, gen_kind=GEN_ZEROS, seed=0):
+        syms = np.ascontiguousarray(syms)
+        n = len(syms)
+        nchunks, out, offsets, lens = _enc_buffers(n, chunk_len)
+        total = u64(0)
+        _check(lib().ans_gpu_loguniform_encode_chunks(self.gpu.h, self.excl_max_bits, _np_ptr(syms), _WIDTH[syms.dtype],
+                                                      n, chunk_len, gen_kind, seed, _np_ptr(out), len(out),
+                                                      _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
+               "ans_gpu_loguniform_encode_chunks")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode_chunks(self, data, offsets, lens, n, chunk_len, dtype=np.uint64, gen_kind=GEN_ZEROS, seed=0):
+        data, offsets, lens = _dec_arrays(data, offsets, lens)
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_loguniform_decode_chunks(self.gpu.h, self.excl_max_bits,
+                                                      _np_ptr(data) if data.size else None, data.size,
+                                                      _np_ptr(offsets), _np_ptr(lens), n, chunk_len, gen_kind, seed,
+                                                      _np_ptr(out), _WIDTH[np.dtype(dtype)]),
+               "ans_gpu_loguniform_decode_chunks")
+        return out[:n]
+
+
+class GpuTableSet:
+    """Independent<Categorical> (src/codec.rs:366-403) on the GPU: a set of Categoricals uploaded
+    once; position k codes with table table_ids[k]."""
+
+    def __init__(self, gpu, categoricals):
+        self.gpu = gpu
+        self.categoricals = list(categoricals)
+        arr = (vp * len(self.categoricals))(*[c.table for c in self.categoricals])
+        h = vp()
+        _check(lib().ans_gpu_tableset_create(gpu.h, arr, len(self.categoricals), ctypes.byref(h)),
+               "ans_gpu_tableset_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            _lib.ans_gpu_tableset_free(h)
+            self.h = None
+
+    def encode_chunks(self, table_ids, syms, chunk_len, gen_kind=GEN_ZEROS, seed=0):
+        syms = np.ascontiguousarray(syms)
+        tids = np.ascontiguousarray(np.asarray(table_ids, dtype=np.uint32))
+        n = len(syms)
+        nchunks, out, offsets, lens = _enc_buffers(n, chunk_len)
+        total = u64(0)
+        _check(lib().ans_gpu_independent_encode_chunks(self.h, _np_ptr(tids), _np_ptr(syms), _WIDTH[syms.dtype], n,
+                                                       chunk_len, gen_kind, seed, _np_ptr(out), len(out),
+                                                       _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
+               "ans_gpu_independent_encode_chunks")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode_chunks(self, table_ids, data, offsets, lens, chunk_len, dtype=np.uint32, gen_kind=GEN_ZEROS, seed=0):
+        data, offsets, lens = _dec_arrays(data, offsets, lens)
+        tids = np.ascontiguousarray(np.asarray(table_ids, dtype=np.uint32))
+        n = len(tids)
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_independent_decode_chunks(self.h, _np_ptr(tids), _np_ptr(data) if data.size else None,
+                                                       data.size, _np_ptr(offsets), _np_ptr(lens), n, chunk_len,
+                                                       gen_kind, seed, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
+               "ans_gpu_independent_decode_chunks")
+        return out[:n]
 
 
 # ============================================================== graph models' bulk caller (section 5)

@@ -59,6 +59,7 @@ struct ans_gpu_table {
     uint32_t lds_bytes;  // 0 = table read from global memory (L2-resident)
     FastTable ft;        // throughput path (ans_fast.hpp) when ft.usable
     void* d_fast;
+    struct ans_gpu_tableset* ts64;  // norm >= 2^32 or nsym > 65536: the exact 64-bit kernels (ans_codecs.hip)
 };
 
 #define ANS_HIP_TRY(expr)                                                                              \
@@ -75,3 +76,22 @@ struct ans_gpu_table {
 int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                                const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
                                uint64_t* lens, uint64_t* total, int gen_kind = ANS_GEN_ZEROS, uint64_t seed = 0);
+
+// The exact 64-bit generic kernels over a table set (ans_codecs.hip): Independent<Categorical>,
+// and IID<Categorical> of tables the u32 kernels do not take (norm >= 2^32, nsym > 65536).
+int ans_tableset_build(ans_gpu* g, const Categorical* const* cats, uint32_t ntables, struct ans_gpu_tableset** out);
+void ans_tableset_destroy(struct ans_gpu_tableset* ts);
+uint64_t ans_tableset_slot_bytes(const struct ans_gpu_tableset* ts, uint64_t chunk_len);
+int ans_tableset_dev_encode(struct ans_gpu_tableset* ts, const void* d_syms, int w, const uint64_t* d_starts, uint64_t n,
+                            uint64_t chunk_len, uint64_t nchunks, uint8_t* d_slots, uint64_t slot_cap,
+                            uint32_t* d_lens, uint32_t* d_status, int gen_kind, uint64_t seed, void* stream);
+int ans_tableset_dev_decode(struct ans_gpu_tableset* ts, const uint8_t* d_in, const uint64_t* d_offsets,
+                            uint64_t slot_cap, const uint32_t* d_lens, const uint64_t* d_starts, uint64_t n,
+                            uint64_t chunk_len, uint64_t nchunks, int gen_kind, uint64_t seed, void* d_syms, int w,
+                            uint32_t* d_status, void* stream);
+int ans_tableset_host_encode(struct ans_gpu_tableset* ts, const void* syms, int w, uint64_t n, uint64_t chunk_len,
+                             const uint64_t* starts, uint64_t nchunks, int gen_kind, uint64_t seed, uint8_t* out,
+                             uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total);
+int ans_tableset_host_decode(struct ans_gpu_tableset* ts, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                             const uint64_t* lens, uint64_t n, uint64_t chunk_len, const uint64_t* starts,
+                             uint64_t nchunks, int gen_kind, uint64_t seed, void* out, int w);

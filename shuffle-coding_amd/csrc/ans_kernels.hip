@@ -1500,8 +1500,22 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
     *out = nullptr;
     const Categorical& cat = tab->cat;
     const uint64_t nsym = cat.masses.size();
-    if (nsym == 0 || nsym > 65536) return ANS_E_NORM_RANGE;
-    if (cat.norm() == 0 || cat.norm() >= (1ull << 32)) return ANS_E_NORM_RANGE;
+    if (nsym == 0 || cat.norm() == 0 || cat.norm() > kMaxMinHead) return ANS_E_NORM_RANGE;
+    if (nsym > 65536 || cat.norm() >= (1ull << 32)) {  // the exact 64-bit kernels (ans_codecs.hip)
+        const Categorical* one = &cat;
+        ans_gpu_tableset* ts = nullptr;
+        const int rc = ans_tableset_build(g, &one, 1, &ts);
+        if (rc) return rc;
+        DevTable t{};
+        t.nsym = nsym > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(nsym);
+        auto* gt = new (std::nothrow) ans_gpu_table{g, t, nullptr, 0, FastTable{}, nullptr, ts};
+        if (!gt) {
+            ans_tableset_destroy(ts);
+            return ANS_E_ALLOC;
+        }
+        *out = gt;
+        return ANS_OK;
+    }
     DevTable t{};
     t.nsym = static_cast<uint32_t>(nsym);
     t.norm = static_cast<uint32_t>(cat.norm());
@@ -1535,7 +1549,7 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
     HIP_TRY(hipMemcpy(static_cast<char*>(mem) + rows_bytes, buckets.data(), bucket_bytes, hipMemcpyHostToDevice));
     t.sym = static_cast<const DevSym*>(mem);
     t.bucket = reinterpret_cast<const uint16_t*>(static_cast<char*>(mem) + rows_bytes);
-    auto* gt = new (std::nothrow) ans_gpu_table{g, t, mem, 0, FastTable{}, nullptr};
+    auto* gt = new (std::nothrow) ans_gpu_table{g, t, mem, 0, FastTable{}, nullptr, nullptr};
     if (!gt) { (void)hipFree(mem); return ANS_E_ALLOC; }
     if (rows_bytes + bucket_bytes <= kLdsTableLimit) gt->lds_bytes = static_cast<uint32_t>(rows_bytes + bucket_bytes);
     const int rc = build_fast_table(gt, cat);
@@ -1550,7 +1564,8 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
 void ans_gpu_table_free(ans_gpu_table* gt) {
     if (!gt) return;
     (void)hipSetDevice(gt->g->device);
-    (void)hipFree(gt->d_mem);
+    if (gt->ts64) ans_tableset_destroy(gt->ts64);
+    if (gt->d_mem) (void)hipFree(gt->d_mem);
     if (gt->d_fast) (void)hipFree(gt->d_fast);
     delete gt;
 }
@@ -1570,6 +1585,10 @@ int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
 
 int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t* slot_cap) {
     if (!gt || !slot_cap) return ANS_E_ARG;
+    if (gt->ts64) {
+        *slot_cap = ans_tableset_slot_bytes(gt->ts64, chunk_len);
+        return ANS_OK;
+    }
     // Bytes of one flattened chunk <= (sum_i log2(norm/p_i) + 1 + L*log2(1+1/K)) / 8 + 8
     // (virtual-bits argument); take every p_i = pmin, plus margin.
     const double per_sym = std::log2(static_cast<double>(gt->t.norm) / static_cast<double>(gt->t.pmin)) +
@@ -1590,6 +1609,9 @@ int ans_dev_encode_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_byte
     if (n && (!d_syms || !d_slots || !d_lens)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
+    if (gt->ts64)
+        return ans_tableset_dev_encode(gt->ts64, d_syms, sym_bytes, nullptr, n, chunk_len, (n + chunk_len - 1) / chunk_len,
+                                       d_slots, slot_cap, d_lens, d_status, gen_kind, seed, s);
     const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
     case 1: return launch_encode<uint8_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s, ini);
@@ -1614,6 +1636,9 @@ int ans_dev_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint6
     if (sym_bytes == 2 && gt->t.nsym > 65536) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
+    if (gt->ts64)
+        return ans_tableset_dev_decode(gt->ts64, d_in, d_offsets, slot_cap, d_lens, nullptr, n, chunk_len,
+                                       (n + chunk_len - 1) / chunk_len, gen_kind, seed, d_syms, sym_bytes, d_status, s);
     const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
     case 1: return launch_decode<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s, ini);
@@ -1634,6 +1659,7 @@ int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n
                     void* stream) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || (n && !d_syms)) return ANS_E_ARG;
+    if (gt->ts64) return ANS_E_NORM_RANGE;  // the synthetic generator reads u32 tables
     if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
@@ -1660,6 +1686,7 @@ int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
                        void* stream) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !d_syms)) return ANS_E_ARG;
+    if (gt->ts64) return ANS_E_NORM_RANGE;  // the sampler reads u32 tables
     if (sym_bytes == 1 && gt->t.nsym > 256) return ANS_E_ARG;
     if (sym_bytes == 2 && gt->t.nsym > 65536) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
@@ -1692,6 +1719,9 @@ int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_
     if (nchunks && (!d_syms || !d_starts || !d_slots || !d_lens)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
+    if (gt->ts64)
+        return ans_tableset_dev_encode(gt->ts64, d_syms, sym_bytes, d_starts, 0, 0, nchunks, d_slots, slot_cap, d_lens,
+                                       d_status, gen_kind, seed, s);
     const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
     case 1: return launch_encode_var<uint8_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
@@ -1716,6 +1746,9 @@ int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const u
     if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = pick(gt, stream);
+    if (gt->ts64)
+        return ans_tableset_dev_decode(gt->ts64, d_in, d_offsets, slot_cap, d_lens, d_starts, 0, 0, nchunks, gen_kind,
+                                       seed, d_syms, sym_bytes, d_status, s);
     const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
     case 1: return launch_decode_var<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
@@ -1849,6 +1882,12 @@ int ans_gpu_encode_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_bytes,
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || !total || !valid_kind(gen_kind)) return ANS_E_ARG;
     const fast::ChunkInit ini{gen_kind, seed};
     if (n && !syms) return ANS_E_ARG;
+    if (gt->ts64) {
+        const uint64_t nc = (n + chunk_len - 1) / chunk_len;
+        if (out && nc && (!offsets || !lens)) return ANS_E_ARG;
+        return ans_tableset_host_encode(gt->ts64, syms, sym_bytes, n, chunk_len, nullptr, nc, gen_kind, seed, out,
+                                        out_cap, offsets, lens, total);
+    }
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (out && nchunks && (!offsets || !lens)) return ANS_E_ARG;
     *total = 0;
@@ -1885,6 +1924,9 @@ int ans_gpu_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_l
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks && (!in || !offsets || !lens || !out)) return ANS_E_ARG;
     if (!valid_kind(gen_kind)) return ANS_E_ARG;
+    if (gt->ts64)
+        return ans_tableset_host_decode(gt->ts64, in, in_len, offsets, lens, n, chunk_len, nullptr, nchunks, gen_kind,
+                                        seed, out, sym_bytes);
     const fast::ChunkInit ini{gen_kind, seed};
     if ((sym_bytes == 1 && gt->t.nsym > 256) || (sym_bytes == 2 && gt->t.nsym > 65536)) return ANS_E_ARG;
     std::vector<uint32_t> l32(nchunks);

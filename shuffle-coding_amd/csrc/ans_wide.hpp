@@ -31,6 +31,7 @@ constexpr uint32_t kWideEncCumMax = (160u * 1024u - kWideEncCum) / 4u;  // stage
 constexpr uint32_t kWideNormMin = 1u << 22;  // one Newton step suffices above (see k_encode_w)
 
 typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 // (cdf(s), cdf(s+1)) from the global cdf array: one 8-B load at a 4-B aligned address
 __device__ __forceinline__ v2u32 cum_pair_global(const uint32_t* cum, uint32_t s) {
@@ -104,8 +105,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     auto request = [&](const uint4& unit, v2u32* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const uint32_t s = min(sym_of<Sym>(unit, j), nsym);
-            lbuf[j] = cum_pair_lds(kWideEncCum, min(s, nl));
+            const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
+            lbuf[j] = cum_pair_lds(kWideEncCum, umin(s, nl));
             if (s >= nl) gbuf[j] = cum_pair_global(gcum, s);
         }
     };
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     auto process = [&](const uint4& unit, const v2u32* lbuf, const v2u32* gbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
-            const bool in_lds = min(sym_of<Sym>(unit, j), nsym) < nl;
+            const bool in_lds = umin(sym_of<Sym>(unit, j), nsym) < nl;
             const v2u32 row = in_lds ? lbuf[j] : gbuf[j];
             const uint32_t cum = row.x, p = row.y - row.x;  // cdf(x), pmf(x) (src/codec.rs:63-64)
             asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(p));
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
             gb = e[1];  // c0..c3 | c4, c5, s0, -
         }
         // LDS prefix (every lane; the bucket index clamped into the prefix)
-        const uint32_t bi = min(cf, cpre - 1) >> shp;
+        const uint32_t bi = umin(cf, cpre - 1) >> shp;
         const uint32_t s0 = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(kWideDecTab + 2 * bi));
         const uint32_t a0 = lcum + 4 * s0;
         const uint32_t c0 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0));
