@@ -302,7 +302,6 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
-    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / kGroupBytes);
     uint8_t* dst = slots + c * slot_cap;
     const uint32_t npages_cap = static_cast<uint32_t>(slot_cap / 64);
     const uint64_t norm = t.norm;
@@ -405,16 +404,17 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 
     // (non-temporal symbol loads / page stores measured 28% SLOWER with rows in global memory)
     auto load_sym = [&](const uint4* p) __attribute__((always_inline)) { return *p; };
-    // groups are walked last to first; group g-1's 64 bytes are requested while g is coded
-    uint4 n0, n1, n2, n3;
-    {
-        const uint4* gsrc = src + 4 * (ngroups - 1);
-        n0 = load_sym(gsrc + 0);
-        n1 = load_sym(gsrc + 1);
-        n2 = load_sym(gsrc + 2);
-        n3 = load_sym(gsrc + 3);
-    }
     if constexpr (kGlobalRows) {
+        // groups are walked last to first; group g-1's 64 bytes are requested while g is coded
+        const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / kGroupBytes);
+        uint4 n0, n1, n2, n3;
+        {
+            const uint4* gsrc = src + 4 * (ngroups - 1);
+            n0 = load_sym(gsrc + 0);
+            n1 = load_sym(gsrc + 1);
+            n2 = load_sym(gsrc + 2);
+            n3 = load_sym(gsrc + 3);
+        }
         EncRow ra[U], rb[U];
         wait_vm();
         request_rows(n3, ra);
@@ -441,23 +441,40 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             process_rows(rb);
         }
     } else {
+        // groups of 128 B (8 units: one whole L2 line per lane and fetch, profiles/r02_hbm_calib.txt)
+        // walked last to first; group g-1 is requested at group g's first point and may stay in
+        // flight through the next one (vmcnt(8): only the older page stores must be done)
+        constexpr int GU = 8;
+        const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
+        uint4 n[GU];
+        {
+            const uint4* gsrc = src + GU * (ngroups - 1);
+#pragma unroll
+            for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
+        }
         for (int g = ngroups - 1; g >= 0; --g) {
-            point();
-            const uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
-            {
-                const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
-                n0 = load_sym(gsrc + 0);
-                n1 = load_sym(gsrc + 1);
-                n2 = load_sym(gsrc + 2);
-                n3 = load_sym(gsrc + 3);
+            uint4 cc[GU];
+#pragma unroll
+            for (int i = 0; i < GU; ++i) cc[i] = n[i];
+#pragma unroll
+            for (int u = GU - 1; u >= 0; --u) {
+                if (u == GU - 2) {  // the page store of the previous point, not the prefetch
+                    wait_vm_n<GU>();
+                    if ((f.pos8 >> 9) > fp) {
+                        if (fp < npages_cap) flush_page(ring, fp, dst);
+                        else over = 1;
+                        ++fp;
+                    }
+                } else {
+                    point();
+                }
+                if (u == GU - 1) {
+                    const uint4* gsrc = src + GU * (g > 0 ? g - 1 : 0);
+#pragma unroll
+                    for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
+                }
+                process(cc[u]);
             }
-            process(c3);
-            point();
-            process(c2);
-            point();
-            process(c1);
-            point();
-            process(c0);
         }
     }
     point();  // the last unit's completed page: the flatten's 8 bytes may reach the ring slot it holds
@@ -543,7 +560,7 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
 // so the whole 160 KiB of LDS holds the 1,024 rings (132 KiB) plus 28 KiB of tables, twice the
 // table room two 512-lane workgroups would leave (finer icdf buckets: C3 resolves every cf with
 // three candidates and compiles no far path).
-__device__ const uint4 kZeroPage[4] = {};  // 64 zero bytes: the Zeros tail generator's pages
+__device__ const uint4 kZeroPage[8] = {};  // 128 zero bytes: the Zeros tail generator's pages
 constexpr int kDecBlock = 1024;
 constexpr int kDecRows = 33;
 constexpr uint32_t kDecRingBytes = kDecRows * kDecBlock * 4;
@@ -556,7 +573,7 @@ static_assert(kDecTableBytes % 256 == 0 && kDecTableBytes / 256 + 16 <= 255, "ri
 struct DecChain {
     uint32_t* ring;  // &ring[0][lane]
     const uint8_t* src;
-    uint4 S[4];
+    uint4 Q[8];  // the aligned page pair (2m, 2m+1) not yet landed: one 128-B L2 line per fetch
     int32_t low, P;
     uint32_t W;
     uint64_t head;
@@ -566,28 +583,41 @@ struct DecChain {
     bool far;
 
     __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kDecBlock]; }
+    // page p (its half of Q) into ring slot p & 1
     __device__ __forceinline__ void put_page(int32_t p) {
         const int32_t r0 = (p & 1) * 16;
+        if (p & 1) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            row(r0 + 4 * k + 0) = S[k].x;
-            row(r0 + 4 * k + 1) = S[k].y;
-            row(r0 + 4 * k + 2) = S[k].z;
-            row(r0 + 4 * k + 3) = S[k].w;
+            for (int k = 0; k < 4; ++k) {
+                row(r0 + 4 * k + 0) = Q[4 + k].x;
+                row(r0 + 4 * k + 1) = Q[4 + k].y;
+                row(r0 + 4 * k + 2) = Q[4 + k].z;
+                row(r0 + 4 * k + 3) = Q[4 + k].w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                row(r0 + 4 * k + 0) = Q[k].x;
+                row(r0 + 4 * k + 1) = Q[k].y;
+                row(r0 + 4 * k + 2) = Q[k].z;
+                row(r0 + 4 * k + 3) = Q[k].w;
+            }
+            row(32) = Q[0].x;
         }
-        if ((p & 1) == 0) row(32) = S[0].x;
     }
-    // pages below 0 come from a zero page in global memory: the same four loads, where a
-    // register zero-fill cost the point 16 v_mov on every wave with one lane at its stream start
+    // pages are fetched as aligned 128-B pairs (2m, 2m+1): a 64-B read leaves the other half of
+    // its 128-B line to be fetched again later (profiles/r02_hbm_calib.txt: 2x the bytes).
+    // Pairs below 0 come from a zero pair in global memory: the same loads, where a register
+    // zero-fill cost a point's worth of v_mov on every wave with one lane at its stream start
     // (global address space: a flat load would also count in lgkmcnt and stall the LDS waits)
-    __device__ __forceinline__ void fetch_page(int32_t p) {
+    __device__ __forceinline__ void fetch_pair(int32_t m) {
         typedef __attribute__((address_space(1))) const v4u32 gv4;
-        const uint4* g = p >= 0 ? reinterpret_cast<const uint4*>(src + 64ll * p) : kZeroPage;
+        const uint4* g = m >= 0 ? reinterpret_cast<const uint4*>(src + 128ll * m) : kZeroPage;
         const gv4* gg = reinterpret_cast<const gv4*>(reinterpret_cast<uintptr_t>(g));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
             const v4u32 v = gg[k];
-            S[k] = make_uint4(v.x, v.y, v.z, v.w);
+            Q[k] = make_uint4(v.x, v.y, v.z, v.w);
         }
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
@@ -600,18 +630,23 @@ struct DecChain {
     }
     // (v_alignbyte_b32 reads only the low two bits of its shift operand: P needs no mask)
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
-    // the top two pages land before decoding starts; the third is requested
+    // the top two pages land before decoding starts; the pair below them is requested
+    // (slot_cap % 128 == 0: the top pair stays inside the slot)
     __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
         src = s;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
-        fetch_page(len > 0 ? top : -1);
+        fetch_pair(len > 0 ? top >> 1 : -1);
         wait_vm();
         put_page(top);
-        fetch_page(top - 1);
-        wait_vm();
-        put_page(top - 1);
+        if (top & 1) {
+            put_page(top - 1);
+            fetch_pair((top >> 1) - 1);  // holds top-3, top-2
+        } else {
+            fetch_pair((top >> 1) - 1);  // holds top-2, top-1
+            wait_vm();
+            put_page(top - 1);  // top-2 stays in the low half
+        }
         low = top - 1;
-        fetch_page(low - 1);
         P = len - 4;
         read_window();
         head = 0;
@@ -629,7 +664,7 @@ struct DecChain {
         if ((((P >> 2) + 1) >> 4) <= low) {  // page low+1 is no longer read: land the one below
             put_page(low - 1);
             --low;
-            fetch_page(low - 1);
+            if (!(low & 1)) fetch_pair((low >> 1) - 1);  // the next page (low-1, odd) opens a new pair
         }
     }
     // phase 1: renorm_up, q/cf, next window

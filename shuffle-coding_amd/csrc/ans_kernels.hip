@@ -422,7 +422,9 @@ inline unsigned grid_for(uint64_t lanes) { return static_cast<unsigned>((lanes +
 // generic kernel.  Both write the same slot layout and identical bytes.
 template <typename Sym>
 uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len, bool decode) {
-    if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % fast::kGroupBytes != 0) return 0;
+    // the LDS-row encoder reads 128-B symbol groups; the decoders store 64-B symbol blocks
+    const uint64_t group = (!decode && !gt->ft.enc_global) ? 128 : fast::kGroupBytes;
+    if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % group != 0) return 0;
     if (decode ? !gt->ft.dec_usable : (sizeof(Sym) == 1 && gt->ft.enc_global)) return 0;
     return n / chunk_len;
 }
@@ -499,7 +501,7 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const FastTable& ft = gt->ft;
     Sym* out = static_cast<Sym*>(d_syms);
     // the fast kernels read the encoder's 64-byte-aligned slot layout only
-    const bool slots = d_offsets == nullptr && slot_cap % 64 == 0;
+    const bool slots = d_offsets == nullptr && slot_cap % 128 == 0;  // page pairs stay inside a slot
     const bool lds_table = slots && fast_chunks<Sym>(gt, n, chunk_len, true) > 0;
     const bool global_table = slots && sizeof(Sym) > 1 && ft.usable && ft.dec_global &&
                               (chunk_len * sizeof(Sym)) % fast::kGroupBytes == 0;

@@ -138,8 +138,15 @@ def test_device_errors_mirror_reference_panics(gpu):
     with pytest.raises(A.AnsError) as e:
         gt.decode_chunks(data[1:], offsets, lens - 1, 8, 8)
     assert e.value.code == A.ANS_E_MISMATCH
+    # norm >= 2^32 codes on the exact 64-bit kernels; only the u32 sampler refuses it
+    wide = A.GpuTable(gpu, A.Categorical([1 << 31, 1 << 31]))
+    data, offsets, lens = wide.encode_chunks(syms % 2, 4)
+    assert np.array_equal(wide.decode_chunks(data, offsets, lens, 8, 4), syms % 2)
     with pytest.raises(A.AnsError) as e:
-        A.GpuTable(gpu, A.Categorical([1 << 31, 1 << 31]))  # norm >= 2^32 unsupported on the GPU
+        wide.sample_chunks(1, 8, 4)
+    assert e.value.code == A.ANS_E_NORM_RANGE
+    with pytest.raises(A.AnsError) as e:
+        A.GpuTable(gpu, A.Categorical([1 << 56, 1]))  # norm > 2^56 breaks the head interval
     assert e.value.code == A.ANS_E_NORM_RANGE
 
 

@@ -25,7 +25,9 @@ import bench  # noqa: E402
 def load(d):
     L = ctypes.CDLL(os.path.join(HERE, "..", "shuffle-coding_amd", d, "libshufflecoding_amd.so"))
     for name, (res, args) in A.SIGNATURES.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)  # an older build may lack newer entry points
+        if f is None:
+            continue
         f.restype = res
         f.argtypes = args
     return L
