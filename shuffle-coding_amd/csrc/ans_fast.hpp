@@ -228,19 +228,50 @@ struct FunnelT {
 };
 using Funnel = FunnelT<kEncRingBase>;
 
-template <bool kNT = false, uint32_t kBase = kEncRingBase>
-__device__ __forceinline__ void flush_page(const RingT<kBase>& ring, uint32_t p, uint8_t* dst) {
-    uint32_t w[16];
+// Completed ring pages leave in aligned pairs, one whole 128-B line per lane: the even page
+// waits in registers for its odd partner.  A lone 64-B store leaves its line half-written in L2
+// until the next page, and the streaming traffic around it evicts such lines in pieces (1.2x
+// the stream's bytes written, profiles/r02c_pmc_c3_summary.txt; the 128-B symbol stores of
+// k_decode write exactly theirs, profiles/r02d_pmc_c3_summary.txt).
+template <uint32_t kBase>
+struct PageOut {
+    uint4 h0, h1, h2, h3;  // page 2m, until 2m+1 completes
+    __device__ __forceinline__ void page(const RingT<kBase>& ring, uint32_t p, uint8_t* dst) {
+        uint32_t w[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = ring.at(static_cast<int32_t>(16 * p + i));
-    uint4* d = reinterpret_cast<uint4*>(dst + 64ull * p);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 v = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-        if (kNT) nt_store(d + q, v);
-        else d[q] = v;
+        for (int i = 0; i < 16; ++i) w[i] = ring.at(static_cast<int32_t>(16 * p + i));
+        const uint4 v0 = make_uint4(w[0], w[1], w[2], w[3]), v1 = make_uint4(w[4], w[5], w[6], w[7]);
+        const uint4 v2 = make_uint4(w[8], w[9], w[10], w[11]), v3 = make_uint4(w[12], w[13], w[14], w[15]);
+        if (p & 1) {
+            uint4* d = reinterpret_cast<uint4*>(dst + 64ull * (p - 1));
+            d[0] = h0;
+            d[1] = h1;
+            d[2] = h2;
+            d[3] = h3;
+            d[4] = v0;
+            d[5] = v1;
+            d[6] = v2;
+            d[7] = v3;
+        }
+        // held unconditionally (an odd page's copy is dead): as an else branch the compiler
+        // merged these writes with the stores above into stores through a selected pointer,
+        // which put the held page in scratch
+        h0 = v0;
+        h1 = v1;
+        h2 = v2;
+        h3 = v3;
     }
-}
+    // after the last page: np pages completed in all (an odd count leaves the last one held)
+    __device__ __forceinline__ void finish(uint32_t np, uint8_t* dst) {
+        if (np & 1) {
+            uint4* d = reinterpret_cast<uint4*>(dst + 64ull * (np - 1));
+            d[0] = h0;
+            d[1] = h1;
+            d[2] = h2;
+            d[3] = h3;
+        }
+    }
+};
 
 // KMAX: most bytes one push can emit (table property); kK32: K < 2^32 (norm > 2^24).
 // kGlobalRows: the rows stay in global memory (alphabets above 256 symbols, e.g. C4's 65,536:
@@ -296,6 +327,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         return r;
     };
     const Ring ring{4 * threadIdx.x};
+    PageOut<kEncRingBase> pout;
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;
@@ -319,7 +351,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto point = [&]() __attribute__((always_inline)) {
         wait_vm();
         if ((f.pos8 >> 9) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
-            if (fp < npages_cap) flush_page(ring, fp, dst);
+            if (fp < npages_cap) pout.page(ring, fp, dst);
             else over = 1;
             ++fp;
         }
@@ -421,8 +453,8 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         for (int g = ngroups - 1; g >= 0; --g) {
             point();
             const uint4 c0 = n0, c1 = n1, c2 = n2;
-            {
-                const uint4* gsrc = src + 4 * (g > 0 ? g - 1 : 0);
+            if (g > 0) {  // (uniform) group 0 has no successor to fetch
+                const uint4* gsrc = src + 4 * (g - 1);
                 n0 = load_sym(gsrc + 0);
                 n1 = load_sym(gsrc + 1);
                 n2 = load_sym(gsrc + 2);
@@ -442,8 +474,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         }
     } else {
         // groups of 128 B (8 units: one whole L2 line per lane and fetch, profiles/r02_hbm_calib.txt)
-        // walked last to first; group g-1 is requested at group g's first point and may stay in
-        // flight through the next one (vmcnt(8): only the older page stores must be done)
+        // walked last to first.  Group g-1 is requested once units 7..4 of group g are coded, so
+        // at most 12 units of symbols are live (the pair of held pages needs those registers),
+        // and stays in flight for four units; no explicit wait: the page stores need none (their
+        // data leaves the registers at issue), and the compiler waits for the loads at first use.
         constexpr int GU = 8;
         const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
         uint4 n[GU];
@@ -452,24 +486,22 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 #pragma unroll
             for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
         }
+        auto flush_ready = [&]() __attribute__((always_inline)) {
+            if ((f.pos8 >> 9) > fp) {
+                if (fp < npages_cap) pout.page(ring, fp, dst);
+                else over = 1;
+                ++fp;
+            }
+        };
         for (int g = ngroups - 1; g >= 0; --g) {
             uint4 cc[GU];
 #pragma unroll
             for (int i = 0; i < GU; ++i) cc[i] = n[i];
 #pragma unroll
             for (int u = GU - 1; u >= 0; --u) {
-                if (u == GU - 2) {  // the page store of the previous point, not the prefetch
-                    wait_vm_n<GU>();
-                    if ((f.pos8 >> 9) > fp) {
-                        if (fp < npages_cap) flush_page(ring, fp, dst);
-                        else over = 1;
-                        ++fp;
-                    }
-                } else {
-                    point();
-                }
-                if (u == GU - 1) {
-                    const uint4* gsrc = src + GU * (g > 0 ? g - 1 : 0);
+                flush_ready();
+                if (u == GU / 2 - 1 && g > 0) {
+                    const uint4* gsrc = src + GU * (g - 1);
 #pragma unroll
                     for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
                 }
@@ -487,9 +519,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     f.finish();
     const uint32_t len = f.len();
     for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
-        if (fp < npages_cap) flush_page(ring, fp, dst);
+        if (fp < npages_cap) pout.page(ring, fp, dst);
         else over = 1;
     }
+    if (!over) pout.finish(fp, dst);
     if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
         uint32_t sym_err = 0;
         for (uint64_t k = 0; k < chunk_len; ++k)
@@ -763,19 +796,19 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 
-    uint4 q0, q1, q2, q3;
+    // symbols leave in whole 128-B lines per lane (eight units): a 64-B store leaves its line
+    // half-written in L2 for a block, where the streaming reads can evict it in pieces
+    uint4 q[8];
     for (int u = 0; u < nunit; ++u) {
         uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             if (j % SPP == 0) {
                 wait_vm();  // point: retire what the previous point issued
-                if (j == 0 && u > 0 && (u & 3) == 0) {  // 64 contiguous bytes per lane
-                    uint4* d = dst + (u - 4);
-                    d[0] = q0;
-                    d[1] = q1;
-                    d[2] = q2;
-                    d[3] = q3;
+                if (j == 0 && u > 0 && (u & 7) == 0) {
+                    uint4* d = dst + (u - 8);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) d[k] = q[k];
                 }
                 ch.point();
             }
@@ -786,20 +819,28 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
             ch.template update<kP24>();
             put_sym<Sym>(outv, j, ch.sx);
         }
-        switch (u & 3) {
-        case 0: q0 = outv; break;
-        case 1: q1 = outv; break;
-        case 2: q2 = outv; break;
-        default: q3 = outv; break;
+        switch (u & 7) {
+        case 0: q[0] = outv; break;
+        case 1: q[1] = outv; break;
+        case 2: q[2] = outv; break;
+        case 3: q[3] = outv; break;
+        case 4: q[4] = outv; break;
+        case 5: q[5] = outv; break;
+        case 6: q[6] = outv; break;
+        default: q[7] = outv; break;
         }
     }
     wait_vm();
-    if (nunit >= 4) {
-        uint4* d = dst + (nunit - 4);
-        d[0] = q0;
-        d[1] = q1;
-        d[2] = q2;
-        d[3] = q3;
+    if (nunit > 0) {  // the last (partial) line: 4 or 8 units (chunk bytes % 64 == 0)
+        const int rem = ((nunit - 1) & 7) + 1;
+        uint4* d = dst + (nunit - rem);
+        if (rem == 8) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[k] = q[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = q[k];
+        }
     }
     // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);

@@ -89,12 +89,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
 
     uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
     FunnelT<kWideRing> f{0, 0, 0, ring.col, ring.col};
+    PageOut<kWideRing> pout;
     uint32_t fp = 0, over = 0;
     uint32_t minmass = ~0u;
 
     auto flush = [&]() __attribute__((always_inline)) {
         if ((f.pos8 >> 9) > fp) {  // at most one page completes per unit (U * KMAX <= 64 bytes)
-            if (fp < npages_cap) flush_page<false, kWideRing>(ring, fp, dst);
+            if (fp < npages_cap) pout.page(ring, fp, dst);
             else over = 1;
             ++fp;
         }
@@ -163,8 +164,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             flush();
             const bool odd = (u & 1) != 0;
             if (u > 0) request(cc[u - 1], odd ? lb : la, odd ? gb : ga);
-            if (u == GU - 1) {
-                const uint4* gsrc = src + GU * (g > 0 ? g - 1 : 0);
+            if (u == GU - 1 && g > 0) {
+                const uint4* gsrc = src + GU * (g - 1);
 #pragma unroll
                 for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
             }
@@ -182,9 +183,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     f.finish();
     const uint32_t len = f.len();
     for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
-        if (fp < npages_cap) flush_page<false, kWideRing>(ring, fp, dst);
+        if (fp < npages_cap) pout.page(ring, fp, dst);
         else over = 1;
     }
+    if (!over) pout.finish(fp, dst);
     if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
         uint32_t sym_err = 0;
         for (uint64_t k = 0; k < chunk_len; ++k)
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     constexpr int UPT = 16 / U;  // units per point: 16 symbols, at most 64 stream bytes
-    const int nblocks = static_cast<int>(chunk_len / (4 * U));  // 64 B of symbols per store
+    const int nunit = static_cast<int>(chunk_len / U);  // a multiple of 4 (chunk bytes % 64 == 0)
     const uint64_t L = t.L;
     const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
@@ -407,37 +409,43 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
         return sx;
     };
 
-    uint4 q[4];
-    for (int b = 0; b < nblocks; ++b) {
+    // symbols leave in whole 128-B lines per lane (eight units; k_decode in ans_fast.hpp): the
+    // last line of a chunk whose bytes are an odd multiple of 64 holds four units
+    uint4 q[8];
+    for (int u0 = 0; u0 < nunit; u0 += 8) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (u % UPT == 0) {
-                wait_vm();  // point: retire what the previous point issued
-                if (u == 0 && b > 0) {  // 64 contiguous bytes of symbols per lane
-                    uint4* d = dst + 4 * (b - 1);
-                    d[0] = q[0];
-                    d[1] = q[1];
-                    d[2] = q[2];
-                    d[3] = q[3];
+        for (int u = 0; u < 8; ++u) {
+            if (u0 + u < nunit) {  // (uniform)
+                if (u % UPT == 0) {
+                    wait_vm();  // point: retire what the previous point issued
+                    if (u == 0 && u0 > 0) {
+                        uint4* d = dst + (u0 - 8);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) d[k] = q[k];
+                    }
+                    ch.point();
                 }
-                ch.point();
-            }
-            uint4 outv = make_uint4(0, 0, 0, 0);
+                uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
-            for (int j = 0; j < U; ++j) {
-                __builtin_amdgcn_sched_barrier(0);
-                put_sym<Sym>(outv, j, step());
+                for (int j = 0; j < U; ++j) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    put_sym<Sym>(outv, j, step());
+                }
+                q[u] = outv;
             }
-            q[u] = outv;
         }
     }
     wait_vm();
-    if (nblocks > 0) {
-        uint4* d = dst + 4 * (nblocks - 1);
-        d[0] = q[0];
-        d[1] = q[1];
-        d[2] = q[2];
-        d[3] = q[3];
+    if (nunit > 0) {
+        const int rem = ((nunit - 1) & 7) + 1;  // 4 or 8
+        uint4* d = dst + (nunit - rem);
+        if (rem == 8) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[k] = q[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = q[k];
+        }
     }
     // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
