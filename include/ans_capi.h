@@ -137,7 +137,7 @@ void ans_gpu_table_free(ans_gpu_table *gt);
 #define ANS_PATH_DEC_LDS 4u     /* fast decoder, icdf buckets in LDS */
 #define ANS_PATH_DEC_GLOBAL 8u  /* fast decoder, icdf buckets in global memory */
 #define ANS_PATH_ENC_WIDE 16u   /* large alphabet, norm >= 2^22: cdf-pair rows, LDS prefix (128-B symbol groups) */
-#define ANS_PATH_DEC_WIDE 32u   /* large alphabet: LDS prefix icdf + global buckets (slot_cap % 128 == 0) */
+#define ANS_PATH_DEC_WIDE 32u   /* large alphabet: LDS prefix icdf + global buckets */
 int ans_gpu_table_paths(const ans_gpu_table *gt, uint32_t *paths);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);
@@ -179,7 +179,8 @@ int ans_gpu_decode_chunks_ex(ans_gpu_table *gt, const uint8_t *in, uint64_t in_l
 int ans_dev_encode_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                           uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status, void *stream);
 /* d_offsets == NULL: chunk j's stream starts at d_in + j*slot_cap (the encoder's layout);
- * otherwise at d_in + d_offsets[j] (e.g. a dense container). */
+ * otherwise at d_in + d_offsets[j] (e.g. a dense container, at any alignment: the fast decoders
+ * read it in place).  Every byte of the aligned 128-B lines holding a stream may be read. */
 int ans_dev_decode_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
                           const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void *d_syms,
                           int sym_bytes, uint32_t *d_status, void *stream);
@@ -231,6 +232,22 @@ int ans_gpu_encode_var_chunks_ex(ans_gpu_table *gt, const void *syms, int sym_by
 int ans_gpu_decode_var_chunks_ex(ans_gpu_table *gt, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
                                  const uint64_t *lens, uint64_t nchunks, const uint64_t *starts, int gen_kind,
                                  uint64_t seed, void *out, int sym_bytes);
+/* Device-resident dense container (the wire format ans_gpu_encode_chunks returns): the chunks
+ * are encoded into d_slots (scratch, nchunks * slot_cap bytes), their lengths scanned into
+ * d_offsets and the streams packed: chunk j at d_out[d_offsets[j] .. + d_lens[j]),
+ * d_offsets[nchunks] = the total.  d_offsets holds ans_dense_offsets_entries(nchunks) entries
+ * (those past nchunks + 1 are scratch).  d_out must hold the total (nchunks * slot_cap always
+ * does); a stream that would end past out_cap is not written and sets ANS_E_LEN in *d_status.
+ * Asynchronous on `stream`.  ans_dev_decode_chunks(_ex) reads the container in place (the
+ * fast decoders fetch the aligned 128-B lines around each stream).  Replaces the encode side of
+ * src/codec.rs:411-419 IID::push over many messages plus their concatenation. */
+uint64_t ans_dense_offsets_entries(uint64_t nchunks);
+int ans_dev_encode_dense(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                         uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens, uint64_t *d_offsets, uint8_t *d_out,
+                         uint64_t out_cap, uint32_t *d_status, void *stream);
+int ans_dev_encode_dense_ex(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                            int gen_kind, uint64_t seed, uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens,
+                            uint64_t *d_offsets, uint8_t *d_out, uint64_t out_cap, uint32_t *d_status, void *stream);
 /* Compacts slot streams into a dense buffer: d_out[d_offsets[j] ..] = slot j. */
 int ans_dev_compact(ans_gpu *g, const uint8_t *d_slots, uint64_t slot_cap, const uint32_t *d_lens,
                     const uint64_t *d_offsets, uint64_t nchunks, uint8_t *d_out, void *stream);

@@ -99,6 +99,9 @@ SIGNATURES = {
     "ans_dev_decode_chunks": (ci, [vp, vp, vp, u64, vp, u64, u64, ci, vp, ci, vp, vp]),
     "ans_dev_gen_iid": (ci, [vp, u64, u64, u64, vp, ci, vp]),
     "ans_dev_compact": (ci, [vp, vp, u64, vp, vp, u64, vp, vp]),
+    "ans_dense_offsets_entries": (u64, [u64]),
+    "ans_dev_encode_dense": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, vp, u64, vp, vp]),
+    "ans_dev_encode_dense_ex": (ci, [vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, vp, u64, vp, vp]),
     "ans_dev_status": (ci, [vp, vp, vp, ctypes.POINTER(ci)]),
     "ans_dev_expand": (ci, [vp, vp, vp, vp, u64, vp, u64, vp]),
     "ans_dev_sample_iid": (ci, [vp, u64, u64, u64, vp, ci, vp]),
@@ -612,6 +615,15 @@ def _dptr(t):
     return t.data_ptr()
 
 
+def _nbytes(t):
+    return t.numel() * t.element_size()
+
+
+def dense_offsets_entries(nchunks):
+    """u64 entries ans_dev_encode_dense needs in d_offsets for nchunks chunks."""
+    return int(lib().ans_dense_offsets_entries(nchunks))
+
+
 def _sptr(stream):
     if stream is None:
         return None
@@ -724,6 +736,14 @@ class GpuTable:
         _check(lib().ans_dev_encode_chunks_ex(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, gen_kind, seed,
                                               _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_status), _sptr(stream)),
                "ans_dev_encode_chunks")
+
+    def dev_encode_dense(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_offsets, d_out,
+                         d_status, stream=None, gen_kind=GEN_ZEROS, seed=0):
+        """Device-resident dense container (ans_dev_encode_dense_ex): d_offsets holds
+        dense_offsets_entries(nchunks) u64 entries; chunk j at d_out[d_offsets[j]:][:d_lens[j]]."""
+        _check(lib().ans_dev_encode_dense_ex(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, gen_kind, seed,
+                                             _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_offsets), _dptr(d_out),
+                                             _nbytes(d_out), _dptr(d_status), _sptr(stream)), "ans_dev_encode_dense")
 
     def dev_decode(self, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status,
                    stream=None, gen_kind=GEN_ZEROS, seed=0):

@@ -580,6 +580,27 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
     cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
 }
 
+// Stream bytes below the stream start (sh > 0: another chunk's bytes in a dense container)
+// read as zeros, the Zeros tail generator's bytes (src/ans.rs:160-170), exactly as below a
+// slot; only a corrupt stream reaches them.  S: one 64-B page at stream position pos.
+__device__ __forceinline__ uint32_t keep_from(uint32_t w, int32_t pos, int32_t sh) {
+    const int32_t k = sh - pos;  // low bytes to clear
+    return k <= 0 ? w : (k >= 4 ? 0u : w & (~0u << (8 * k)));
+}
+__device__ __forceinline__ uint4 keep4(const uint4& v, int32_t pos, int32_t sh) {
+    return make_uint4(keep_from(v.x, pos, sh), keep_from(v.y, pos + 4, sh), keep_from(v.z, pos + 8, sh),
+                      keep_from(v.w, pos + 12, sh));
+}
+// (by value: a pointer into a register array that differs between branches puts it in scratch)
+__device__ __forceinline__ void clear_below(uint4& a0, uint4& a1, uint4& a2, uint4& a3, int32_t pos, int32_t sh) {
+    if (__builtin_expect(pos < sh, 0)) {
+        a0 = keep4(a0, pos, sh);
+        a1 = keep4(a1, pos + 16, sh);
+        a2 = keep4(a2, pos + 32, sh);
+        a3 = keep4(a3, pos + 48, sh);
+    }
+}
+
 // ====================================================================== decode
 // One decode chain = one chunk, read from the end.  P is the stream position minus 4: the
 // window W = stream bytes [P, P+4) (byte P+3 on top) comes from ring dwords y = P>>2 and y+1
@@ -607,7 +628,7 @@ struct DecChain {
     uint32_t* ring;  // &ring[0][lane]
     const uint8_t* src;
     uint4 Q[8];  // the aligned page pair (2m, 2m+1) not yet landed: one 128-B L2 line per fetch
-    int32_t low, P;
+    int32_t low, P, sh;  // sh: the stream start within its 128-B line
     uint32_t W;
     uint64_t head;
     // per-step values between the phases
@@ -619,24 +640,22 @@ struct DecChain {
     // page p (its half of Q) into ring slot p & 1
     __device__ __forceinline__ void put_page(int32_t p) {
         const int32_t r0 = (p & 1) * 16;
+        uint4 a0, a1, a2, a3;
         if (p & 1) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                row(r0 + 4 * k + 0) = Q[4 + k].x;
-                row(r0 + 4 * k + 1) = Q[4 + k].y;
-                row(r0 + 4 * k + 2) = Q[4 + k].z;
-                row(r0 + 4 * k + 3) = Q[4 + k].w;
-            }
+            a0 = Q[4], a1 = Q[5], a2 = Q[6], a3 = Q[7];
         } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                row(r0 + 4 * k + 0) = Q[k].x;
-                row(r0 + 4 * k + 1) = Q[k].y;
-                row(r0 + 4 * k + 2) = Q[k].z;
-                row(r0 + 4 * k + 3) = Q[k].w;
-            }
-            row(32) = Q[0].x;
+            a0 = Q[0], a1 = Q[1], a2 = Q[2], a3 = Q[3];
         }
+        clear_below(a0, a1, a2, a3, 64 * p, sh);
+        const uint4 a[4] = {a0, a1, a2, a3};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            row(r0 + 4 * k + 0) = a[k].x;
+            row(r0 + 4 * k + 1) = a[k].y;
+            row(r0 + 4 * k + 2) = a[k].z;
+            row(r0 + 4 * k + 3) = a[k].w;
+        }
+        if (!(p & 1)) row(32) = a0.x;
     }
     // pages are fetched as aligned 128-B pairs (2m, 2m+1): a 64-B read leaves the other half of
     // its 128-B line to be fetched again later (profiles/r02_hbm_calib.txt: 2x the bytes).
@@ -663,10 +682,15 @@ struct DecChain {
     }
     // (v_alignbyte_b32 reads only the low two bits of its shift operand: P needs no mask)
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
-    // the top two pages land before decoding starts; the pair below them is requested
-    // (slot_cap % 128 == 0: the top pair stays inside the slot)
-    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
-        src = s;
+    // the top two pages land before decoding starts; the pair below them is requested.
+    // s: the stream's first byte, at any alignment (a dense container).  Positions count from
+    // the 128-B line holding it (base = s - sh), so every fetch is whole aligned lines, read
+    // only from lines that hold stream bytes; the sh bytes below the stream (another chunk's)
+    // are reached only by a corrupt stream, which the final position check reports.
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t slen) {
+        sh = static_cast<int32_t>(reinterpret_cast<uintptr_t>(s) & 127u);
+        src = s - sh;
+        const int32_t len = slen + sh;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
         fetch_pair(len > 0 ? top >> 1 : -1);
         wait_vm();
@@ -758,6 +782,7 @@ struct DecChain {
 // kP24: every mass is below 2^24 (DecChain::update).  kJ4: some pop can pull 4 bytes (kmax = 4).
 template <typename Sym, int SPP, bool kFar, bool kP24, bool kJ4>
 __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                      const uint64_t* __restrict__ offsets,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
                                                       uint32_t* __restrict__ status, ChunkInit ini) {
@@ -786,14 +811,14 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
     // a stream longer than its slot is foreign or corrupt: its pages would lie past the slot
-    if (lens[c] > slot_cap) {
+    if (!offsets && lens[c] > slot_cap) {
         atomicOr(status, 1u << ANS_E_LEN);
         return;
     }
     DecChain ch;
     ch.ring = reinterpret_cast<uint32_t*>(lds + kDecTableBytes) + threadIdx.x;
     ch.col = 4 * threadIdx.x;
-    ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
+    ch.start(slots + (offsets ? offsets[c] : c * slot_cap), static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 
     // symbols leave in whole 128-B lines per lane (eight units): a 64-B store leaves its line
@@ -844,7 +869,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     }
     // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
-    const int32_t remaining = ch.P + 4;  // < 0: generated
+    const int32_t remaining = ch.P + 4 - ch.sh;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
@@ -866,7 +891,7 @@ struct DecChainG {
     uint32_t* ring;  // &ring[0][lane]
     const uint8_t* src;
     uint4 S0[4], S1[4];  // pages low-1 and low-2, in flight
-    int32_t low, P;
+    int32_t low, P, sh;  // sh: the stream start within its 128-B line
     uint32_t wx, wy, W;
     uint64_t head;
     uint64_t qq;
@@ -874,7 +899,8 @@ struct DecChainG {
     bool far;
 
     __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kBlock]; }
-    __device__ __forceinline__ void put_page(int32_t p, const uint4* S) {
+    __device__ __forceinline__ void put_page(int32_t p, uint4* S) {
+        clear_below(S[0], S[1], S[2], S[3], 64 * p, sh);
         const int32_t r0 = (p & 3) * 16;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -903,8 +929,14 @@ struct DecChainG {
     }
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }  // low 2 bits used
     // the top four pages land before decoding starts; the next two are requested
-    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
-        src = s;
+    // s: the stream's first byte, at any alignment (a dense container).  Positions count from
+    // the 128-B line holding it (base = s - sh), so every fetch is whole aligned lines, read
+    // only from lines that hold stream bytes; the sh bytes below the stream (another chunk's)
+    // are reached only by a corrupt stream, which the final position check reports.
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t slen) {
+        sh = static_cast<int32_t>(reinterpret_cast<uintptr_t>(s) & 127u);
+        src = s - sh;
+        const int32_t len = slen + sh;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
         fetch_page(len > 0 ? top : -1, S0);
         fetch_page(top - 1, S1);
@@ -980,7 +1012,8 @@ struct DecChainG {
 
 template <typename Sym>
 __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8_t* __restrict__ slots,
-                                                        uint64_t slot_cap, const uint32_t* __restrict__ lens,
+                                                        uint64_t slot_cap, const uint64_t* __restrict__ offsets,
+                                                        const uint32_t* __restrict__ lens,
                                                         uint64_t chunk_len, uint64_t nfull, int gen_kind,
                                                         Sym* __restrict__ out, uint32_t* __restrict__ status,
                                                         ChunkInit ini) {
@@ -998,13 +1031,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
     const uint32_t shift = t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
-    if (lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
+    if (!offsets && lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
         atomicOr(status, 1u << ANS_E_LEN);
         return;
     }
     DecChainG ch;
     ch.ring = reinterpret_cast<uint32_t*>(lds) + threadIdx.x;
-    ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
+    ch.start(slots + (offsets ? offsets[c] : c * slot_cap), static_cast<int32_t>(lens[c]));
     ch.pull_until(L);
 
     uint4 q[4];
@@ -1041,7 +1074,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
         d[3] = q[3];
     }
     ch.pull_until(kMaxMinHead);
-    const int32_t remaining = ch.P + 4;
+    const int32_t remaining = ch.P + 4 - ch.sh;
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }

@@ -384,6 +384,54 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8
     if (lane < len - 4 * nd) dst[4 * nd + lane] = src[4 * nd + lane];
 }
 
+// One wave packs one stream from a 16-B-aligned source (a slot) to any destination in whole
+// aligned 16-B stores: destination block j (of the 16-B-aligned line holding dst, dsh = dst & 15)
+// takes stream bytes [16j - dsh, 16j - dsh + 16), i.e. source blocks j-1 and j funnelled by
+// v_alignbyte at a wave-uniform dword step and byte shift.  The first and last blocks may hold
+// a neighbouring stream's bytes: those are written byte by byte (no store touches a byte
+// outside the stream, so neighbouring waves never race).  Only source blocks holding stream
+// bytes are read.
+__device__ __forceinline__ void wave_pack(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
+                                          uint32_t lane) {
+    if (len == 0) return;
+    const uint32_t dsh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst) & 15);
+    uint8_t* dbase = dst - dsh;
+    const uint4* s16 = reinterpret_cast<const uint4*>(src);
+    const uint32_t nblk = (dsh + len + 15) / 16;
+    const uint32_t bs = (16u - dsh) & 3u;         // byte shift inside the 32-B window
+    const uint32_t i0 = (16u - dsh) >> 2;         // first window dword of an output block
+    for (uint32_t j = lane; j < nblk; j += 64) {
+        const uint4 a = j > 0 ? s16[j - 1] : make_uint4(0, 0, 0, 0);
+        const uint4 b = 16 * j < len ? s16[j] : make_uint4(0, 0, 0, 0);  // only blocks holding stream bytes
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t o[4];
+        // i0 is wave-uniform: a scalar branch picks constant register indices
+        switch (i0) {
+#define PACK_CASE(I)                                                                 \
+    case I:                                                                          \
+        for (int k = 0; k < 4; ++k)                                                  \
+            o[k] = (I + k + 1 < 8) ? __builtin_amdgcn_alignbyte(w[(I + k + 1) & 7], w[I + k], bs) : w[I + k]; \
+        break;
+            PACK_CASE(0)
+            PACK_CASE(1)
+            PACK_CASE(2)
+            PACK_CASE(3)
+            default:
+                for (int k = 0; k < 4; ++k) o[k] = w[4 + k];  // dsh = 0: block j itself
+#undef PACK_CASE
+        }
+        const uint32_t lo = j == 0 ? dsh : 0u;                           // first byte of the stream here
+        const uint32_t hi = min(16u, dsh + len - 16u * j);               // one past its last
+        if (lo == 0 && hi == 16) {
+            *reinterpret_cast<uint4*>(dbase + 16ull * j) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (uint32_t t = 0; t < 16; ++t)
+                if (t >= lo && t < hi) dbase[16ull * j + t] = static_cast<uint8_t>(o[t >> 2] >> (8 * (t & 3)));
+        }
+    }
+}
+
 // One wave per chunk copies its slot into the dense container.
 __global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                     const uint32_t* __restrict__ lens,
@@ -394,7 +442,9 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ 
     if (c >= nchunks) return;
     const uint8_t* s = slots + c * slot_cap;
     uint8_t* d = out + offsets[c];
-    wave_copy(d, s, static_cast<uint32_t>(min<uint64_t>(lens[c], slot_cap)), lane);  // never past the slot
+    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(lens[c], slot_cap));  // never past the slot
+    if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) wave_pack(d, s, len, lane);
+    else wave_copy(d, s, len, lane);
 }
 
 // One wave per chunk copies a dense-container stream into its slot (the inverse of k_compact).
@@ -407,6 +457,89 @@ __global__ __launch_bounds__(kBlock) void k_expand(const uint8_t* __restrict__ i
     const uint8_t* s = in + offsets[c];
     uint8_t* d = slots + c * slot_cap;
     wave_copy(d, s, lens[c], lane);
+}
+
+// ---- device-resident dense container (include/ans_capi.h ans_dev_encode_dense_ex)
+// Exclusive scan of the stream lengths in tiles of 4,096 chunks (1,024 threads x 4, a
+// 64-lane shuffle scan per wave, the 16 wave totals through LDS): each tile leaves its local
+// offsets and its total; k_scan_tile_sums scans the totals in place (one workgroup); then
+// k_compact_dense adds its tile's prefix, publishes the final offset and packs the stream.
+// Lengths are clamped to the slot like k_compact's copies, so offsets and bytes agree.
+constexpr uint32_t kScanTile = 4096;
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_tiles(const uint32_t* __restrict__ lens, uint64_t n, uint64_t slot_cap,
+                                                     uint64_t* __restrict__ offs, uint64_t* __restrict__ tile_sum) {
+    __shared__ uint64_t wsum[16];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kScanTile + 4 * threadIdx.x;
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k < n ? min<uint64_t>(lens[i0 + k], slot_cap) : 0;
+    const uint64_t t = v[0] + v[1] + v[2] + v[3];
+    const uint64_t incl = wave_incl_scan(t, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t run = incl - t;
+    for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (i0 + k < n) offs[i0 + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 1023) tile_sum[blockIdx.x] = run;  // the tile's total
+}
+
+__global__ __launch_bounds__(1024) void k_scan_tile_sums(uint64_t* __restrict__ tile_sum, uint64_t ntiles,
+                                                         uint64_t* __restrict__ total) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry = 0;
+    for (uint64_t b = 0; b < ntiles; b += 1024) {
+        __syncthreads();  // carry written, last round's wsum reads done
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t t = i < ntiles ? tile_sum[i] : 0;
+        const uint64_t incl = wave_incl_scan(t, lane);
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint64_t pre = carry + incl - t;
+        for (uint32_t w = 0; w < wave; ++w) pre += wsum[w];
+        if (i < ntiles) tile_sum[i] = pre;
+        __syncthreads();  // every carry read done
+        if (threadIdx.x == 1023) carry = pre + t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// One wave per chunk: offset = local + tile prefix; the stream is packed unless it would end
+// past out_cap (ANS_E_LEN).
+__global__ __launch_bounds__(kBlock) void k_compact_dense(const uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                          const uint32_t* __restrict__ lens, uint64_t* __restrict__ offs,
+                                                          const uint64_t* __restrict__ tile_pre, uint64_t nchunks,
+                                                          uint8_t* __restrict__ out, uint64_t out_cap,
+                                                          uint32_t* __restrict__ status) {
+    const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
+    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(lens[c], slot_cap));
+    const uint64_t off = offs[c] + tile_pre[c / kScanTile];
+    if (lane == 0) offs[c] = off;  // (every lane has read offs[c]: one load instruction)
+    if (off + len > out_cap) {
+        if (lane == 0) atomicOr(status, 1u << ANS_E_LEN);
+        return;
+    }
+    const uint8_t* src = slots + c * slot_cap;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) wave_pack(out + off, src, len, lane);
+    else wave_copy(out + off, src, len, lane);
 }
 
 // ------------------------------------------------------------------ launch helpers
@@ -500,10 +633,10 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const DevTable& t = gt->t;
     const FastTable& ft = gt->ft;
     Sym* out = static_cast<Sym*>(d_syms);
-    // the fast kernels read the encoder's 64-byte-aligned slot layout only
-    const bool slots = d_offsets == nullptr && slot_cap % 128 == 0;  // page pairs stay inside a slot
-    const bool lds_table = slots && fast_chunks<Sym>(gt, n, chunk_len, true) > 0;
-    const bool global_table = slots && sizeof(Sym) > 1 && ft.usable && ft.dec_global &&
+    // the fast kernels read whole aligned 128-B lines around each stream, from the slot layout
+    // or a dense container alike (fast::DecChain::start)
+    const bool lds_table = fast_chunks<Sym>(gt, n, chunk_len, true) > 0;
+    const bool global_table = sizeof(Sym) > 1 && ft.usable && ft.dec_global &&
                               (chunk_len * sizeof(Sym)) % fast::kGroupBytes == 0;
     const uint64_t nfull = (lds_table || global_table) ? n / chunk_len : 0;
     if (nfull) {
@@ -511,15 +644,15 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         constexpr int U = 16 / sizeof(Sym);
         if (global_table) {
             if constexpr (sizeof(Sym) > 1) {
-                if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0 && slot_cap % 128 == 0)
-                    fast::k_decode_w<Sym><<<grid, fast::kBlock, 160 * 1024, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
+                    fast::k_decode_w<Sym><<<grid, fast::kBlock, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                 else
-                    fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                    fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
             }
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
-#define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
+#define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
 #define DEC_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true, J4); else DEC(SPP, FAR, false, J4)
 #define DEC_J(SPP, FAR) if (ft.kmax >= 4) { DEC_P(SPP, FAR, true); } else { DEC_P(SPP, FAR, false); }
             if (U * ft.kmax > 60) {  // (kmax = 4)
@@ -1864,6 +1997,38 @@ int ans_dev_expand(ans_gpu* g, const uint8_t* d_in, const uint64_t* d_offsets, c
     k_expand<<<grid_for(nchunks * 64), kBlock, 0, s>>>(d_in, d_offsets, d_lens, nchunks, d_slots, slot_cap);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
+}
+
+uint64_t ans_dense_offsets_entries(uint64_t nchunks) { return nchunks + 1 + (nchunks + kScanTile - 1) / kScanTile; }
+
+int ans_dev_encode_dense_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                            int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
+                            uint64_t* d_offsets, uint8_t* d_out, uint64_t out_cap, uint32_t* d_status, void* stream) {
+    if (n && (!d_offsets || !d_out)) return ANS_E_ARG;
+    int rc = ans_dev_encode_chunks_ex(gt, d_syms, sym_bytes, n, chunk_len, gen_kind, seed, d_slots, slot_cap, d_lens,
+                                      d_status, stream);
+    if (rc) return rc;
+    const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
+    const hipStream_t s = pick(gt, stream);
+    if (nchunks == 0) {
+        if (d_offsets) HIP_TRY(hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), s));
+        return ANS_OK;
+    }
+    const uint64_t ntiles = (nchunks + kScanTile - 1) / kScanTile;
+    uint64_t* tile = d_offsets + nchunks + 1;
+    k_scan_tiles<<<static_cast<unsigned>(ntiles), 1024, 0, s>>>(d_lens, nchunks, slot_cap, d_offsets, tile);
+    k_scan_tile_sums<<<1, 1024, 0, s>>>(tile, ntiles, d_offsets + nchunks);
+    k_compact_dense<<<grid_for(nchunks * 64), kBlock, 0, s>>>(d_slots, slot_cap, d_lens, d_offsets, tile, nchunks,
+                                                              d_out, out_cap, d_status);
+    HIP_TRY(hipGetLastError());
+    return ANS_OK;
+}
+
+int ans_dev_encode_dense(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                         uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint64_t* d_offsets, uint8_t* d_out,
+                         uint64_t out_cap, uint32_t* d_status, void* stream) {
+    return ans_dev_encode_dense_ex(gt, d_syms, sym_bytes, n, chunk_len, ANS_GEN_ZEROS, 0, d_slots, slot_cap, d_lens,
+                                   d_offsets, d_out, out_cap, d_status, stream);
 }
 
 int ans_dev_status(ans_gpu* g, const uint32_t* d_status, void* stream, int* status) {

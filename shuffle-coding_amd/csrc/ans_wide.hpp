@@ -219,7 +219,7 @@ struct DecChainW {
     uint32_t col;  // 4 * lane
     const uint8_t* src;
     uint4 Q[8];    // the page pair (2m, 2m+1) not yet landed
-    int32_t low, P;
+    int32_t low, P, sh;  // sh: the stream start within its 128-B line
     uint32_t wx, wy, W;
     uint64_t head;
     uint64_t qq;
@@ -242,24 +242,22 @@ struct DecChainW {
     // page p (its half of Q) into ring slot p & 1
     __device__ __forceinline__ void land(int32_t p) {
         const int32_t r0 = (p & 1) * 16;
+        uint4 a0, a1, a2, a3;
         if (p & 1) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                row(r0 + 4 * k + 0) = Q[4 + k].x;
-                row(r0 + 4 * k + 1) = Q[4 + k].y;
-                row(r0 + 4 * k + 2) = Q[4 + k].z;
-                row(r0 + 4 * k + 3) = Q[4 + k].w;
-            }
+            a0 = Q[4], a1 = Q[5], a2 = Q[6], a3 = Q[7];
         } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                row(r0 + 4 * k + 0) = Q[k].x;
-                row(r0 + 4 * k + 1) = Q[k].y;
-                row(r0 + 4 * k + 2) = Q[k].z;
-                row(r0 + 4 * k + 3) = Q[k].w;
-            }
-            row(32) = Q[0].x;
+            a0 = Q[0], a1 = Q[1], a2 = Q[2], a3 = Q[3];
         }
+        clear_below(a0, a1, a2, a3, 64 * p, sh);
+        const uint4 a[4] = {a0, a1, a2, a3};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            row(r0 + 4 * k + 0) = a[k].x;
+            row(r0 + 4 * k + 1) = a[k].y;
+            row(r0 + 4 * k + 2) = a[k].z;
+            row(r0 + 4 * k + 3) = a[k].w;
+        }
+        if (!(p & 1)) row(32) = a0.x;
     }
     __device__ __forceinline__ void read_window() {
         const uint32_t a = ((static_cast<uint32_t>(P) << 9) & 0xF800u) | col;  // row (P >> 2) & 31
@@ -268,8 +266,14 @@ struct DecChainW {
     }
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
     // the top two pages land before decoding starts; the pair below them is requested
-    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
-        src = s;
+    // s: the stream's first byte, at any alignment (a dense container).  Positions count from
+    // the 128-B line holding it (base = s - sh), so every fetch is whole aligned lines, read
+    // only from lines that hold stream bytes; the sh bytes below the stream (another chunk's)
+    // are reached only by a corrupt stream, which the final position check reports.
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t slen) {
+        sh = static_cast<int32_t>(reinterpret_cast<uintptr_t>(s) & 127u);
+        src = s - sh;
+        const int32_t len = slen + sh;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
         fetch_pair(len > 0 ? top >> 1 : -1);
         wait_vm();
@@ -315,7 +319,8 @@ struct DecChainW {
 
 template <typename Sym>
 __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
-                                                         uint64_t slot_cap, const uint32_t* __restrict__ lens,
+                                                         uint64_t slot_cap, const uint64_t* __restrict__ offsets,
+                                                         const uint32_t* __restrict__ lens,
                                                          uint64_t chunk_len, uint64_t nfull, int gen_kind,
                                                          Sym* __restrict__ out, uint32_t* __restrict__ status,
                                                          ChunkInit ini) {
@@ -330,7 +335,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;  // no barrier below: lanes are independent
-    if (lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
+    if (!offsets && lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
         atomicOr(status, 1u << ANS_E_LEN);
         return;
     }
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
 
     DecChainW ch;
     ch.col = 4 * threadIdx.x;
-    ch.start(slots + c * slot_cap, static_cast<int32_t>(lens[c]));
+    ch.start(slots + (offsets ? offsets[c] : c * slot_cap), static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 
     auto step = [&]() __attribute__((always_inline)) {
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
     }
     // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
-    const int32_t remaining = ch.P + 4;  // < 0: generated
+    const int32_t remaining = ch.P + 4 - ch.sh;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }

@@ -262,18 +262,29 @@ def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed):
     assert gpu.status(status, stream) == 0
     assert torch.equal(out, syms), "lossless round trip"
     del out
-    # the dense container (the wire format) of every chunk
+    # the dense container (the wire format) of every chunk, built on the device
+    # (ans_dev_encode_dense: encode + length scan + packing) and decoded in place
     l64 = lens.to(torch.int64)
-    offs = torch.cumsum(l64, 0) - l64
-    total = int(l64.sum().item())
-    dense = torch.empty(total, dtype=torch.uint8, device="cuda")
-    gpu.compact(slots, cap, lens, offs, nchunks, dense, stream)
+    offs = torch.empty(A.dense_offsets_entries(nchunks), dtype=torch.int64, device="cuda")
+    lens2 = torch.zeros_like(lens)
+    dense = torch.empty(nchunks * cap, dtype=torch.uint8, device="cuda")
+    gt.dev_encode_dense(syms, sym_bytes, n, chunk_len, slots, cap, lens2, offs, dense, status, stream)
+    del slots
+    assert torch.equal(lens2, lens), "dense encode: the same stream lengths"
+    assert torch.equal(offs[:nchunks], torch.cumsum(l64, 0) - l64), "exclusive scan of the lengths"
+    total = int(offs[nchunks].item())
+    assert total == int(l64.sum().item())
+    out = torch.empty_like(syms)
+    gt.dev_decode(dense, offs, cap, lens, n, chunk_len, out, sym_bytes, status, stream)
+    assert gpu.status(status, stream) == 0
+    assert torch.equal(out, syms), "lossless round trip from the dense container"
+    del out
     torch.cuda.synchronize()
     torch.cuda.set_stream(torch.cuda.default_stream())
     lens_h = l64.cpu().numpy()
-    offs_h = offs.cpu().numpy()
-    dense_h = dense.cpu().numpy()
-    del slots, dense
+    offs_h = offs[:nchunks].cpu().numpy()
+    dense_h = dense[:total].cpu().numpy()
+    del dense
     # the device generator is the oracle's (spot check; the streams below depend on all of it)
     ref = orc.gen_iid(masses, seed, n - 4096, 4096)
     assert np.array_equal(syms[n - 4096:].cpu().numpy().astype(np.int64) & ((1 << (8 * sym_bytes)) - 1), ref)
@@ -300,10 +311,36 @@ def test_c4_shard_u16_round_trip(gpu):
     assert 1.9 < total / (1 << 27) < 2.1
 
 
+def test_compact_packs_exact_bytes(gpu):
+    """ans_dev_compact (16-B packing with byte-exact first/last blocks): streams of every length
+    class (0, 1, 15, 16, 17, ..., a whole slot) at every destination alignment land byte-exact,
+    and no byte outside a stream is written (the gaps keep their sentinel)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(5)
+    cap, nchunks = 256, 600
+    lens_h = rng.integers(0, cap + 1, nchunks).astype(np.int64)
+    lens_h[:8] = [0, 1, 15, 16, 17, 31, 33, cap]
+    gaps = rng.integers(0, 40, nchunks)
+    offs_h = np.cumsum(gaps + np.concatenate([[0], lens_h[:-1]])).astype(np.int64)
+    slots_h = rng.integers(0, 256, nchunks * cap, dtype=np.uint8)
+    total = int(offs_h[-1] + lens_h[-1]) + 64
+    want = np.full(total, 0xAB, np.uint8)
+    for j in range(nchunks):
+        want[offs_h[j]:offs_h[j] + lens_h[j]] = slots_h[j * cap:j * cap + lens_h[j]]
+    slots = torch.from_numpy(slots_h).cuda()
+    lens = torch.from_numpy(lens_h.astype(np.int32)).cuda()
+    offs = torch.from_numpy(offs_h).cuda()
+    dense = torch.full((total,), 0xAB, dtype=torch.uint8, device="cuda")
+    gpu.compact(slots, cap, lens, offs, nchunks, dense)
+    torch.cuda.synchronize()
+    assert np.array_equal(dense.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("sym_bytes", [1, 2])
 def test_dense_and_slot_layouts_decode_alike(gpu, sym_bytes):
-    """ans_dev_decode_chunks on the dense container (explicit offsets: generic kernel) and on
-    the encoder's slot layout (fast kernel) give the same symbols and status."""
+    """ans_dev_decode_chunks on the dense container (explicit offsets, streams at any alignment,
+    read in place) and on the encoder's slot layout give the same symbols and status, also for
+    a corrupt stream that reads below its start (zeros there, not the previous chunk's bytes)."""
     torch = pytest.importorskip("torch")
     dt = {1: torch.uint8, 2: torch.int16}[sym_bytes]
     masses = A.c3_masses()
