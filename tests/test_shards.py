@@ -1,7 +1,9 @@
 """The N>1 path: chunk sharding across ranks on CPU with gloo, world_size 2.
 
-Each rank codes its contiguous chunk range; rank 0 assembles the container.  The result
-must equal one process coding everything (chunk streams are independent messages).  The
+Each rank codes its contiguous chunk range; the container is assembled either in rank 0's
+memory (point-to-point pieces at scanned offsets) or in one file each rank writes its own
+range of.  The result must equal one process coding everything (chunk streams are
+independent messages).  The
 per-shard coder here is the oracle standing in for GpuTable.encode_chunks/decode_chunks
 (no GPU in this container); the GPU versions of those calls are covered by
 tests/test_gpu_parity.py.
@@ -37,7 +39,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, masses, syms, chunk_len, q):
+def _worker(rank, world, port, masses, syms, chunk_len, q, mode, tmp):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -45,7 +47,19 @@ def _worker(rank, world, port, masses, syms, chunk_len, q):
     try:
         enc = lambda s, L: orc.encode_chunks(masses, s, L)  # noqa: E731
         dec = lambda d, o, l, n, L: orc.decode_chunks(masses, d, o, l, n, L)  # noqa: E731
-        got = shards.encode_distributed(enc, syms, chunk_len)
+        if mode == "file":  # every rank writes its own range of one container file
+            path = os.path.join(tmp, "container.bin")
+            _, offsets, lens = shards.encode_distributed(enc, syms, chunk_len, out=path)
+            sym_path = os.path.join(tmp, "symbols.bin")
+            shards.decode_distributed(dec, path, offsets, lens, len(syms), chunk_len, out=sym_path)
+            if rank == 0:
+                with open(path, "rb") as f:
+                    data = f.read()
+                q.put(("enc", data, offsets.tolist(), lens.tolist()))
+                q.put(("dec", np.fromfile(sym_path, np.uint8).tolist()))
+            return
+        # in memory: point-to-point pieces of 1000 bytes into rank 0's preallocated buffers
+        got = shards.encode_distributed(enc, syms, chunk_len, piece=1000)
         if rank == 0:
             data, offsets, lens = got
             q.put(("enc", data.tobytes(), offsets.tolist(), lens.tolist()))
@@ -53,15 +67,16 @@ def _worker(rank, world, port, masses, syms, chunk_len, q):
             data = offsets = lens = None
         obj = [data, offsets, lens]
         dist.broadcast_object_list(obj, src=0)
-        back = shards.decode_distributed(dec, obj[0], obj[1], obj[2], len(syms), chunk_len)
+        back = shards.decode_distributed(dec, obj[0], obj[1], obj[2], len(syms), chunk_len, piece=1000)
         if rank == 0:
             q.put(("dec", back.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,chunk_len", [(50_000, 4096), (4096 * 5, 4096), (999, 10)])
-def test_two_rank_gloo_matches_single_process(n, chunk_len):
+@pytest.mark.parametrize("mode", ["memory", "file"])
+@pytest.mark.parametrize("n,chunk_len", [(50_000, 4096), (4096 * 5, 4096), (999, 10), (5, 10)])
+def test_two_rank_gloo_matches_single_process(n, chunk_len, mode, tmp_path):
     import torch.multiprocessing as mp
 
     masses = np.asarray([1 + (i * 7919) % 4000 for i in range(256)], np.uint64)
@@ -69,7 +84,8 @@ def test_two_rank_gloo_matches_single_process(n, chunk_len):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, masses, syms, chunk_len, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, masses, syms, chunk_len, q, mode, str(tmp_path)))
+             for r in range(2)]
     for p in procs:
         p.start()
     msgs = [q.get(timeout=120) for _ in range(2)]
