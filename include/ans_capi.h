@@ -138,6 +138,8 @@ void ans_gpu_table_free(ans_gpu_table *gt);
 #define ANS_PATH_DEC_GLOBAL 8u  /* fast decoder, icdf buckets in global memory */
 #define ANS_PATH_ENC_WIDE 16u   /* large alphabet, norm >= 2^22: cdf-pair rows, LDS prefix (128-B symbol groups) */
 #define ANS_PATH_DEC_WIDE 32u   /* large alphabet: LDS prefix icdf + global buckets */
+#define ANS_PATH_DEC_COMPACT 64u /* ... whose global buckets are 16 B (u16 candidate offsets) */
+#define ANS_PATH_ENC_PACKED 128u /* large-alphabet encoder with the packed (u32 base + u16) LDS prefix */
 int ans_gpu_table_paths(const ans_gpu_table *gt, uint32_t *paths);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);

@@ -28,6 +28,8 @@ ANS_E_NORM_RANGE, ANS_E_DEVICE, ANS_E_ALLOC, ANS_E_ARG, ANS_E_MISMATCH = 5, 6, 7
 GEN_ZEROS, GEN_EMPTY, GEN_RANDOM = 0, 1, 2
 ANS_PATH_ENC_LDS, ANS_PATH_ENC_GLOBAL, ANS_PATH_DEC_LDS, ANS_PATH_DEC_GLOBAL = 1, 2, 4, 8
 ANS_PATH_ENC_WIDE, ANS_PATH_DEC_WIDE = 16, 32
+ANS_PATH_DEC_COMPACT = 64
+ANS_PATH_ENC_PACKED = 128
 MAX_MIN_HEAD = 1 << 56
 MAX_SIZE = MAX_MIN_HEAD >> 10
 

@@ -585,14 +585,16 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         }
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
-                const size_t wlds = fast::kWideEncCum + 4 * (ft.enc_nl + 1);
-#define ENCW(KM, K32) fast::k_encode_w<Sym, KM, K32><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+                const size_t wlds = fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
+#define ENCW2(KM, K32, PK) fast::k_encode_w<Sym, KM, K32, PK><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+#define ENCW(KM, K32) if (ft.enc_pack) ENCW2(KM, K32, true); else ENCW2(KM, K32, false)
                 switch (ft.kmax) {
                 case 1: case 2: if (k32) ENCW(2, true); else ENCW(2, false); break;
                 case 3: if (k32) ENCW(3, true); else ENCW(3, false); break;
                 default: if (k32) ENCW(4, true); else ENCW(4, false); break;
                 }
 #undef ENCW
+#undef ENCW2
             } else if (ft.enc_global) {
                 ENC_KMAX(true, false)
             } else if (ft.enc_rare) {
@@ -644,8 +646,11 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         constexpr int U = 16 / sizeof(Sym);
         if (global_table) {
             if constexpr (sizeof(Sym) > 1) {
-                if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
-                    fast::k_decode_w<Sym><<<grid, fast::kBlock, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                const unsigned wgrid = static_cast<unsigned>((nfull + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
+                if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0)
+                    fast::k_decode_w<Sym, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                else if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
+                    fast::k_decode_w<Sym, false><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                 else
                     fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
             }
@@ -834,8 +839,66 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         }
     }
     ft.dec_global = !ft.dec_usable;
+    // compact 16-B buckets for k_decode_w: the finest width with at most 2^17 buckets (2 MiB),
+    // if every bucket's five candidate offsets fit u16
+    std::vector<DecBucketC> decc;
+    if (ft.dec_global) {
+        uint32_t cs = 0;
+        while (((static_cast<uint64_t>(t.norm) - 1) >> cs) + 1 > (1ull << 17)) ++cs;
+        const uint32_t ncb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> cs) + 1);
+        decc.resize(ncb);
+        bool fits = true;
+        for (uint32_t j = 0; j < ncb && fits; ++j) {
+            const uint32_t s0 = static_cast<uint32_t>(cat.icdf(static_cast<uint64_t>(j) << cs).first);
+            DecBucketC& d = decc[j];
+            d.c0 = cum[s0];
+            d.s0 = static_cast<uint16_t>(s0);
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t off = cum[s0 + 1 + k] - cum[s0];
+                if (off > 0xFFFFu) fits = false;
+                d.d[k] = static_cast<uint16_t>(off);
+            }
+        }
+        if (fits) {
+            ft.dec_c = 1;
+            ft.dec_c_shift = cs;
+        } else {
+            decc.clear();
+        }
+    }
     ft.enc_wide = ft.enc_global && t.norm >= fast::kWideNormMin;
     ft.enc_nl = std::min<uint32_t>(nsym, fast::kWideEncCumMax - 1);
+    // the packed prefix (ans_table.hpp enc_pack): the longest multiple of 16 symbols whose image
+    // fits the same LDS and whose in-block offsets fit u16; used when it is longer
+    std::vector<uint32_t> pack_img;
+    if (ft.enc_wide) {
+        const uint32_t budget = 4 * fast::kWideEncCumMax;
+        auto img_bytes = [](uint32_t nl) {
+            const uint32_t ooff = 4 * ((nl >> 4) + 2);
+            return (ooff + 2 * (nl + 2) + 3) & ~3u;
+        };
+        uint32_t nlp = 0;
+        while (nlp + 16 <= nsym && img_bytes(nlp + 16) <= budget) {
+            bool fits = true;
+            for (uint32_t k = nlp; k < nlp + 16 && fits; ++k) fits = cum[k + 1] - cum[nlp] <= 0xFFFFu || ((k + 1) & 15) == 0;
+            if (!fits) break;
+            nlp += 16;
+        }
+        if (nlp > ft.enc_nl) {
+            const uint32_t ooff = 4 * ((nlp >> 4) + 2);
+            pack_img.assign(img_bytes(nlp) / 4, 0);
+            for (uint32_t k = 0; k < (nlp >> 4) + 2; ++k) pack_img[k] = cum[std::min<uint32_t>(16 * k, nsym + 5)];
+            auto* o16 = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(pack_img.data()) + ooff);
+            for (uint32_t k = 0; k < nlp + 2; ++k) {
+                const uint32_t sidx = std::min<uint32_t>(k, nsym + 5);
+                o16[k] = k < nlp ? static_cast<uint16_t>(cum[sidx] - cum[16 * (k >> 4)]) : 0;
+            }
+            ft.enc_pack = 1;
+            ft.enc_nl = nlp;
+            ft.enc_pack_ooff = ooff;
+            ft.enc_pack_bytes = img_bytes(nlp);
+        }
+    }
     // k_decode_w's LDS prefix: for each bucket width 2^shp, the longest prefix of symbols whose
     // bucket starts (u16) and cdf fit beside the ring; keep the width whose prefix covers the most
     // probability among those whose cf needs a fifth candidate at most 0.1% of the time
@@ -908,9 +971,13 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const size_t o_decg = o_cum + ((sizeof(uint32_t) * cum.size() + 255) & ~size_t(255));
     const size_t o_ws0 = o_decg + ((decg_b + 255) & ~size_t(255));
     const size_t ws0_b = sizeof(uint16_t) * wide_s0.size();
+    const size_t o_decc = o_ws0 + ((ws0_b + 255) & ~size_t(255));
+    const size_t decc_b = sizeof(DecBucketC) * decc.size();
+    const size_t o_pack = o_decc + ((decc_b + 255) & ~size_t(255));
+    const size_t pack_b = sizeof(uint32_t) * pack_img.size();
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
-    HIP_TRY(hipMalloc(&mem, o_ws0 + ws0_b + 16));
+    HIP_TRY(hipMalloc(&mem, o_pack + pack_b + 16));
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
@@ -926,6 +993,10 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     HIP_TRY(hipMemcpy(base + o_cum, cum.data(), sizeof(uint32_t) * cum.size(), hipMemcpyHostToDevice));
     if (decg_b) HIP_TRY(hipMemcpy(base + o_decg, decg.data(), decg_b, hipMemcpyHostToDevice));
     if (ws0_b) HIP_TRY(hipMemcpy(base + o_ws0, wide_s0.data(), ws0_b, hipMemcpyHostToDevice));
+    if (decc_b) HIP_TRY(hipMemcpy(base + o_decc, decc.data(), decc_b, hipMemcpyHostToDevice));
+    ft.dbkt_c = reinterpret_cast<const DecBucketC*>(base + o_decc);
+    if (pack_b) HIP_TRY(hipMemcpy(base + o_pack, pack_img.data(), pack_b, hipMemcpyHostToDevice));
+    ft.enc_pack_img = reinterpret_cast<const uint32_t*>(base + o_pack);
     ft.dec_w_s0 = reinterpret_cast<const uint16_t*>(base + o_ws0);
     ft.dbkt_g = reinterpret_cast<const DecBucketG*>(base + o_decg);
     ft.enc = reinterpret_cast<const EncRow*>(base);
@@ -1714,6 +1785,8 @@ int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
     if (ft.usable && ft.dec_global) p |= ANS_PATH_DEC_GLOBAL;
     if (ft.usable && ft.enc_wide) p |= ANS_PATH_ENC_WIDE;
     if (ft.usable && ft.dec_wide) p |= ANS_PATH_DEC_WIDE;
+    if (ft.usable && ft.dec_wide && ft.dec_c) p |= ANS_PATH_DEC_COMPACT;
+    if (ft.usable && ft.enc_wide && ft.enc_pack) p |= ANS_PATH_ENC_PACKED;
     *paths = p;
     return ANS_OK;
 }

@@ -66,6 +66,15 @@ struct alignas(16) DecBucketG {
     uint32_t s0;
     uint32_t pad;
 };
+// Compact large-alphabet bucket (16 B, one global load): c0 = cdf(s0) and the offsets
+// d[k] = cdf(s0 + 1 + k) - c0, k = 0..4, as u16 (built only when every offset fits), so the
+// same five candidates as DecBucketG in one L2 request instead of two.
+struct alignas(16) DecBucketC {
+    uint32_t c0;
+    uint16_t s0;
+    uint16_t d[5];
+};
+static_assert(sizeof(DecBucketC) == 16, "one 16-B load");
 struct FastTable {
     const EncRow* enc;        // enc_rows = nsym + 1 rows (last = zero-mass sentinel)
     const DecBucket* dbkt;    // dec_buckets entries, then dec_buckets u32 s0 values (16-aligned region)
@@ -102,6 +111,17 @@ struct FastTable {
     uint32_t dec_w_shp;
     uint32_t dec_w_nbp;
     uint32_t dec_w_cum_off;    // LDS offset of the cdf prefix from the s0 array (16-aligned)
+    // k_encode_w with a packed LDS prefix (enc_pack): cdf(s) = B[s >> 4] + O[s] for s < enc_nl,
+    // B (u32, enc_nl/16 + 2 entries) at the image's start and O (u16, enc_nl + 2 entries) at
+    // byte enc_pack_ooff: 2.25 B per symbol instead of 4, so a longer prefix fits
+    const uint32_t* enc_pack_img;
+    uint32_t enc_pack;
+    uint32_t enc_pack_ooff;
+    uint32_t enc_pack_bytes;  // image bytes (a multiple of 4), staged into LDS as u32 words
+    // k_decode_w past the prefix: compact buckets (dec_c) of width 2^dec_c_shift, else dbkt_g
+    const DecBucketC* dbkt_c;
+    uint32_t dec_c;
+    uint32_t dec_c_shift;
 };
 
 }  // namespace shuffle_coding

@@ -59,7 +59,10 @@ __device__ __forceinline__ double rcp_newton(uint32_t p) {
 // Groups of 128 B of symbols (8 units of 16 B) per lane, walked last to first; each unit's rows
 // are requested at the point before it (LDS or global, per lane), so their latency hides behind
 // one unit of work.  Points and the byte funnel are ans_fast.hpp's.
-template <typename Sym, int KMAX, bool kK32>
+// kPack: the LDS prefix is the packed image (FastTable::enc_pack): a row costs a ds_read2_b32
+// of two block bases and two ds_read_u16 of offsets plus ~6 VALU, for ~1.8x the prefix (67%
+// of C4's symbols instead of 37%; the rest is the L2 request each).
+template <typename Sym, int KMAX, bool kK32, bool kPack>
 __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
                                                          uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                          uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
@@ -67,7 +70,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     extern __shared__ __align__(16) unsigned char lds[];
     {
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideEncCum);
-        for (uint32_t i = threadIdx.x; i <= t.enc_nl; i += kBlock) lc[i] = t.cum[i];
+        if constexpr (kPack) {
+            for (uint32_t i = threadIdx.x; i < t.enc_pack_bytes / 4; i += kBlock) lc[i] = t.enc_pack_img[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i <= t.enc_nl; i += kBlock) lc[i] = t.cum[i];
+        }
     }
     const RingT<kWideRing> ring{4 * threadIdx.x};
     __syncthreads();
@@ -103,12 +110,30 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     // a unit's rows: every lane reads the LDS pair of min(s, nl) (always in range) and the lanes
     // whose symbol lies past the prefix also load the global pair, into separate registers (a
     // shared destination would make each LDS read wait for every outstanding global load)
-    auto request = [&](const uint4& unit, v2u32* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
+    // (packed: lbuf holds the two block bases and the two offsets, combined in process)
+    using LRow = typename std::conditional<kPack, uint4, v2u32>::type;
+    const uint32_t ooff = kWideEncCum + t.enc_pack_ooff;
+    auto request = [&](const uint4& unit, LRow* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
-            lbuf[j] = cum_pair_lds(kWideEncCum, umin(s, nl));
+            const uint32_t sp = umin(s, nl);
+            if constexpr (kPack) {
+                const v2u32 b = cum_pair_lds(kWideEncCum, sp >> 4);
+                const uint32_t oa = ooff + 2 * sp;
+                lbuf[j] = make_uint4(b.x, b.y, *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa)),
+                                     *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa + 2)));
+            } else {
+                lbuf[j] = cum_pair_lds(kWideEncCum, sp);
+            }
             if (s >= nl) gbuf[j] = cum_pair_global(gcum, s);
+        }
+    };
+    auto lrow = [&](const LRow& r, uint32_t s) __attribute__((always_inline)) {
+        if constexpr (kPack) {  // cdf(s) = B[s >> 4] + O[s]; cdf(s + 1) from the next base at a block end
+            return v2u32{r.x + r.z, ((s + 1) & 15u) ? r.x + r.w : r.y};
+        } else {
+            return r;
         }
     };
     // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
@@ -119,11 +144,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 8u : 0u;
         return k;
     };
-    auto process = [&](const uint4& unit, const v2u32* lbuf, const v2u32* gbuf) __attribute__((always_inline)) {
+    auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
-            const bool in_lds = umin(sym_of<Sym>(unit, j), nsym) < nl;
-            const v2u32 row = in_lds ? lbuf[j] : gbuf[j];
+            const uint32_t sj = umin(sym_of<Sym>(unit, j), nsym);
+            const bool in_lds = sj < nl;
+            const v2u32 row = in_lds ? lrow(lbuf[j], sj) : gbuf[j];
             const uint32_t cum = row.x, p = row.y - row.x;  // cdf(x), pmf(x) (src/codec.rs:63-64)
             asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(p));
             const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
@@ -148,7 +174,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
 #pragma unroll
         for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
     }
-    v2u32 la[U], lb[U], ga[U], gb[U];
+    LRow la[U], lb[U];
+    v2u32 ga[U], gb[U];
     wait_vm();
     request(n[GU - 1], la, ga);
     for (int g = ngroups - 1; g >= 0; --g) {
@@ -210,7 +237,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
 // one global page fetch per 128 B exposes its HBM latency once per ~64 symbols (gfx9 retires
 // vector-memory operations in issue order, so a page fetch delays the next bucket load).
 constexpr int kWideDecRows = 33;
-constexpr uint32_t kWideDecTab = kWideDecRows * kBlock * 4;  // 67,584 B of ring, then the tables
+// 512 lanes: 1,024 (four waves per SIMD, 25 KiB of tables) measured 40% slower on C4, its
+// smaller LDS prefix sending more lookups to L2
+constexpr uint32_t kWideDecLanes = 512;
+constexpr uint32_t kWideDecRowShift = 11;  // log2 of a ring row's bytes
+static_assert((1u << kWideDecRowShift) == kWideDecLanes * 4, "row bytes");
+constexpr uint32_t kWideDecTab = kWideDecRows * kWideDecLanes * 4;  // 67,584 B of ring, then the tables
 static_assert(kWideDecTab % 256 == 0, "table base");
 constexpr uint32_t kWideDecTabBytes = 160u * 1024u - kWideDecTab;
 __device__ const uint4 kZeroPair[8] = {};  // 128 zero bytes: pages below the stream start
@@ -227,7 +259,7 @@ struct DecChainW {
     bool far;
 
     __device__ __forceinline__ lds_u32& row(int32_t r) const {
-        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(static_cast<uint32_t>(r) * (kBlock * 4) + col));
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>((static_cast<uint32_t>(r) << kWideDecRowShift) + col));
     }
     __device__ __forceinline__ void fetch_pair(int32_t m) {
         typedef __attribute__((address_space(1))) const v4u32 gv4;
@@ -260,9 +292,9 @@ struct DecChainW {
         if (!(p & 1)) row(32) = a0.x;
     }
     __device__ __forceinline__ void read_window() {
-        const uint32_t a = ((static_cast<uint32_t>(P) << 9) & 0xF800u) | col;  // row (P >> 2) & 31
+        const uint32_t a = ((static_cast<uint32_t>(P) << (kWideDecRowShift - 2)) & (31u << kWideDecRowShift)) | col;  // row (P >> 2) & 31
         wy = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a));
-        wx = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a + kBlock * 4));
+        wx = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a + kWideDecLanes * 4));
     }
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
     // the top two pages land before decoding starts; the pair below them is requested
@@ -317,8 +349,10 @@ struct DecChainW {
     __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
 };
 
-template <typename Sym>
-__global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
+// kCompact: the buckets past the prefix are DecBucketC (16 B: one L2 request per symbol;
+// C4 is bound by the L2's request rate, profiles/r02f_pmc_c4_summary.txt), else DecBucketG.
+template <typename Sym, bool kCompact>
+__global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
                                                          uint64_t slot_cap, const uint64_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ lens,
                                                          uint64_t chunk_len, uint64_t nfull, int gen_kind,
@@ -328,12 +362,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
     {  // the prefix tables: bucket s0 values (u16), then cdf(0 .. nlp + 5)
         const uint32_t* gs = reinterpret_cast<const uint32_t*>(t.dec_w_s0);
         uint32_t* ls = reinterpret_cast<uint32_t*>(lds + kWideDecTab);
-        for (uint32_t i = threadIdx.x; i < (t.dec_w_nbp + 1) / 2; i += kBlock) ls[i] = gs[i];
+        for (uint32_t i = threadIdx.x; i < (t.dec_w_nbp + 1) / 2; i += kWideDecLanes) ls[i] = gs[i];
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideDecTab + t.dec_w_cum_off);
-        for (uint32_t i = threadIdx.x; i <= t.dec_w_nlp + 5; i += kBlock) lc[i] = t.cum[i];
+        for (uint32_t i = threadIdx.x; i <= t.dec_w_nlp + 5; i += kWideDecLanes) lc[i] = t.cum[i];
     }
     __syncthreads();
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kWideDecLanes + threadIdx.x;
     if (c >= nfull) return;  // no barrier below: lanes are independent
     if (!offsets && lens[c] > slot_cap) {  // foreign or corrupt stream: its pages would lie past the slot
         atomicOr(status, 1u << ANS_E_LEN);
@@ -350,6 +384,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
     const uint32_t shift = t.dec_shift, shp = t.dec_w_shp, cpre = t.dec_w_cpre;
     const uint32_t lcum = kWideDecTab + t.dec_w_cum_off;  // LDS byte address of cdf(0)
     const DecBucketG* __restrict__ bkt = t.dbkt_g;
+    const DecBucketC* __restrict__ bktc = t.dbkt_c;
+    const uint32_t cshift = t.dec_c_shift;
     const uint32_t* __restrict__ gcum = t.cum;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
@@ -365,9 +401,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
         // global bucket (lanes past the prefix only): issued first, the longer round trip
         uint4 ga = make_uint4(0, 0, 0, 0), gb = make_uint4(0, 0, 0, 0);
         if (!pre) {
-            const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
-            ga = e[0];
-            gb = e[1];  // c0..c3 | c4, c5, s0, -
+            if constexpr (kCompact) {
+                ga = *reinterpret_cast<const uint4*>(bktc + (cf >> cshift));  // c0 | s0, d0 | d1, d2 | d3, d4
+            } else {
+                const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
+                ga = e[0];
+                gb = e[1];  // c0..c3 | c4, c5, s0, -
+            }
         }
         // LDS prefix (every lane; the bucket index clamped into the prefix)
         const uint32_t bi = umin(cf, cpre - 1) >> shp;
@@ -386,6 +426,18 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_w(FastTable t, const uint8
             nxt = b3 ? c4 : (b2 ? c3 : (b1 ? c2 : c1));
             sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
             far = cf >= c4;
+        } else if constexpr (kCompact) {
+            asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w));
+            const uint32_t rel = cf - ga.x;  // cf - cdf(s0)
+            const uint32_t d0 = ga.y >> 16, d1 = ga.z & 0xFFFFu, d2 = ga.z >> 16, d3 = ga.w & 0xFFFFu,
+                           d4 = ga.w >> 16;
+            const bool b1 = rel >= d0, b2 = rel >= d1, b3 = rel >= d2, b4 = rel >= d3;
+            const uint32_t lo = b4 ? d3 : (b3 ? d2 : (b2 ? d1 : (b1 ? d0 : 0u)));
+            const uint32_t hi = b4 ? d4 : (b3 ? d3 : (b2 ? d2 : (b1 ? d1 : d0)));
+            cum = ga.x + lo;
+            nxt = ga.x + hi;
+            sx = (ga.y & 0xFFFFu) + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
+            far = rel >= d4;
         } else {
             asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w), "v"(gb.x), "v"(gb.y), "v"(gb.z));
             const bool b1 = cf >= ga.y, b2 = cf >= ga.z, b3 = cf >= ga.w, b4 = cf >= gb.x;
