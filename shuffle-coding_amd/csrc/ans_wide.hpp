@@ -349,9 +349,11 @@ struct DecChainW {
     __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
 };
 
-// kCompact: the buckets past the prefix are DecBucketC (16 B: one L2 request per symbol;
-// C4 is bound by the L2's request rate, profiles/r02f_pmc_c4_summary.txt), else DecBucketG.
-template <typename Sym, bool kCompact>
+// kCompact: the global buckets are DecBucketC (16 B, one L2 request), else DecBucketG (32 B).
+// kPrefix: resolve cf below dec_w_cpre from the LDS prefix, else every lookup is global (the
+// compact tables: a wave step waits on L2 as soon as one of its 64 lanes misses the prefix,
+// which for C4 is nearly every step, so the prefix only added VALU to the chain).
+template <typename Sym, bool kCompact, bool kPrefix>
 __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
                                                          uint64_t slot_cap, const uint64_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ lens,
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
                                                          Sym* __restrict__ out, uint32_t* __restrict__ status,
                                                          ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
-    {  // the prefix tables: bucket s0 values (u16), then cdf(0 .. nlp + 5)
+    if (kPrefix) {  // the prefix tables: bucket s0 values (u16), then cdf(0 .. nlp + 5)
         const uint32_t* gs = reinterpret_cast<const uint32_t*>(t.dec_w_s0);
         uint32_t* ls = reinterpret_cast<uint32_t*>(lds + kWideDecTab);
         for (uint32_t i = threadIdx.x; i < (t.dec_w_nbp + 1) / 2; i += kWideDecLanes) ls[i] = gs[i];
@@ -397,7 +399,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
     auto step = [&]() __attribute__((always_inline)) {
         ch.renorm_div(L, hL8, norm, rcp_norm);
         const uint32_t cf = ch.cf;
-        const bool pre = cf < cpre;
+        const bool pre = kPrefix && cf < cpre;
         // global bucket (lanes past the prefix only): issued first, the longer round trip
         uint4 ga = make_uint4(0, 0, 0, 0), gb = make_uint4(0, 0, 0, 0);
         if (!pre) {
