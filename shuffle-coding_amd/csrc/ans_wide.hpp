@@ -346,7 +346,7 @@ struct DecChainW {
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
     }
-    __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
+    __device__ __forceinline__ void update(uint32_t p, uint32_t r) { head = qq * p + r; }
 };
 
 // kCompact: the global buckets are DecBucketC (16 B, one L2 request), else DecBucketG (32 B).
@@ -420,37 +420,43 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
         const uint32_t c2 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 8));
         const uint32_t c3 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 12));
         const uint32_t c4 = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a0 + 16));
-        uint32_t cum, nxt, sx;
+        // the pop's p = pmf(s) and r = cf - cdf(s) (src/codec.rs:65-68)
+        uint32_t p, r, sx;
         bool far;
         if (pre) {
             const bool b1 = cf >= c1, b2 = cf >= c2, b3 = cf >= c3;
-            cum = b3 ? c3 : (b2 ? c2 : (b1 ? c1 : c0));
-            nxt = b3 ? c4 : (b2 ? c3 : (b1 ? c2 : c1));
+            const uint32_t cum = b3 ? c3 : (b2 ? c2 : (b1 ? c1 : c0));
+            const uint32_t nxt = b3 ? c4 : (b2 ? c3 : (b1 ? c2 : c1));
+            p = nxt - cum;
+            r = cf - cum;
             sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u);
             far = cf >= c4;
         } else if constexpr (kCompact) {
             asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w));
-            const uint32_t rel = cf - ga.x;  // cf - cdf(s0)
+            const uint32_t rel = cf - ga.x;  // cf - cdf(s0); the candidates' offsets are cdf - cdf(s0)
             const uint32_t d0 = ga.y >> 16, d1 = ga.z & 0xFFFFu, d2 = ga.z >> 16, d3 = ga.w & 0xFFFFu,
                            d4 = ga.w >> 16;
             const bool b1 = rel >= d0, b2 = rel >= d1, b3 = rel >= d2, b4 = rel >= d3;
             const uint32_t lo = b4 ? d3 : (b3 ? d2 : (b2 ? d1 : (b1 ? d0 : 0u)));
             const uint32_t hi = b4 ? d4 : (b3 ? d3 : (b2 ? d2 : (b1 ? d1 : d0)));
-            cum = ga.x + lo;
-            nxt = ga.x + hi;
+            p = hi - lo;
+            r = rel - lo;
             sx = (ga.y & 0xFFFFu) + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
             far = rel >= d4;
         } else {
             asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w), "v"(gb.x), "v"(gb.y), "v"(gb.z));
             const bool b1 = cf >= ga.y, b2 = cf >= ga.z, b3 = cf >= ga.w, b4 = cf >= gb.x;
-            cum = b4 ? gb.x : (b3 ? ga.w : (b2 ? ga.z : (b1 ? ga.y : ga.x)));
-            nxt = b4 ? gb.y : (b3 ? gb.x : (b2 ? ga.w : (b1 ? ga.z : ga.y)));
+            const uint32_t cum = b4 ? gb.x : (b3 ? ga.w : (b2 ? ga.z : (b1 ? ga.y : ga.x)));
+            const uint32_t nxt = b4 ? gb.y : (b3 ? gb.x : (b2 ? ga.w : (b1 ? ga.z : ga.y)));
+            p = nxt - cum;
+            r = cf - cum;
             sx = gb.z + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
             far = cf >= gb.y;
         }
         if (__builtin_expect(__any(far), 0)) {
             if (far) {  // more boundaries than candidates: scan the cdf (src/codec.rs:66 partition_point)
                 sx += 1;
+                uint32_t cum, nxt;
                 if (pre) {
                     while (cf >= *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(lcum + 4 * (sx + 1)))) ++sx;
                     cum = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(lcum + 4 * sx));
@@ -460,11 +466,11 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
                     cum = gcum[sx];
                     nxt = gcum[sx + 1];
                 }
+                p = nxt - cum;
+                r = cf - cum;
             }
         }
-        ch.cum = cum;
-        ch.nxt = nxt;
-        ch.update();  // head = p*q + r (src/ans.rs:113-114)
+        ch.update(p, r);  // head = p*q + r (src/ans.rs:113-114)
         return sx;
     };
 
