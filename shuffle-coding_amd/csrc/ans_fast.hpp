@@ -752,6 +752,34 @@ struct DecChain {
         sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u);
         far = cf >= c.w;
     }
+    // lookup for tables with no far case (kFar = false): the two selects in VOP2 form, each
+    // compare's mask in VCC (the compiler keeps both masks in SGPR pairs for the unit's end and
+    // emits every select, and the symbol's two 0/1 terms, as 64-bit-encoded VOP3), and the
+    // symbol offset t = b1 + b2 by a v_addc whose carry-in is the second mask; sx = s0 + t is
+    // formed off the chain.  s_nop 1: VALU-written VCC read as a lane mask (gfx950 hazard).
+    __device__ __forceinline__ void lookup_nofar(uint32_t shift, uint32_t one) {
+        const uint32_t bi = cf >> shift;
+        const uint64_t ca = lds_ld64(bi << 3), cb = lds_ld64((bi << 3) + 8 * kDecNbMax);
+        const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0Off));
+        uint32_t t;
+        asm volatile(
+            "v_cmp_ge_u32 vcc, %[cf], %[c1]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32 %[cum], %[c0], %[c1], vcc\n\t"
+            "v_cndmask_b32 %[nxt], %[c1], %[c2], vcc\n\t"
+            "v_cndmask_b32 %[t], 0, %[one], vcc\n\t"
+            "v_cmp_ge_u32 vcc, %[cf], %[c2]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32 %[cum], %[cum], %[c2], vcc\n\t"
+            "v_cndmask_b32 %[nxt], %[nxt], %[c3], vcc\n\t"
+            "v_addc_co_u32 %[t], vcc, 0, %[t], vcc"
+            : [cum] "=&v"(cum), [nxt] "=&v"(nxt), [t] "=&v"(t)
+            : [cf] "v"(cf), [c0] "v"(lo32(ca)), [c1] "v"(hi32(ca)), [c2] "v"(lo32(cb)), [c3] "v"(hi32(cb)),
+              [one] "v"(one)
+            : "vcc");
+        sx = s0 + t;
+        far = false;
+    }
     __device__ __forceinline__ void lookup_far(const uint32_t* lcum) {  // 3+ boundaries in the bucket
         if (far) {
             sx += 1;
@@ -808,6 +836,8 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
+    uint32_t one = 1;
+    asm volatile("" : "+v"(one));  // a VGPR holding 1 (lookup_nofar's VOP2 select source)
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
     // a stream longer than its slot is foreign or corrupt: its pages would lie past the slot
@@ -839,8 +869,12 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
             }
             __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
             ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
-            ch.lookup(shift);
-            if (kFar && __builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+            if constexpr (kFar) {
+                ch.lookup(shift);
+                if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+            } else {
+                ch.lookup_nofar(shift, one);
+            }
             ch.template update<kP24>();
             put_sym<Sym>(outv, j, ch.sx);
         }
