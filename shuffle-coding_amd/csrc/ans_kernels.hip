@@ -553,6 +553,145 @@ inline unsigned grid_for(uint64_t lanes) { return static_cast<unsigned>((lanes +
 // Full chunks whose symbols tile into 16-byte units go to the fast kernel when the table
 // allows it; everything else (ragged last chunk, odd chunk lengths, other tables) to the
 // generic kernel.  Both write the same slot layout and identical bytes.
+// ---- staged chunks: ragged (chunk bytes not a multiple of the fast kernels' 128-B groups, e.g.
+// C2's 1,563 u16 symbols) and variable-length chunks through the fast large-alphabet kernels.
+// Chunk c's symbols are copied to the start of a stride of lpad symbols (lpad * w a multiple
+// of 128), k_encode_w / k_decode_w run with kVar (their first-coded group partial), and decoded
+// symbols are copied back.  One thread per 16-B unit of the staging buffer.
+template <typename Sym>
+struct ChunkSpan {  // chunk c = symbols [start(c), start(c) + len(c)) of the caller's array
+    const uint64_t* starts;  // variable chunks (nchunks + 1 entries), or nullptr
+    uint64_t chunk_len, n;   // fixed chunks (the last one may be short)
+    __device__ __forceinline__ uint64_t start(uint64_t c) const { return starts ? starts[c] : c * chunk_len; }
+    __device__ __forceinline__ uint64_t len(uint64_t c) const {
+        return starts ? starts[c + 1] - starts[c] : min(chunk_len, n - c * chunk_len);
+    }
+};
+
+template <typename Sym>
+__global__ __launch_bounds__(kBlock) void k_stage(const Sym* __restrict__ src, ChunkSpan<Sym> span, uint64_t nchunks,
+                                                  uint64_t lpad, Sym* __restrict__ stage, uint32_t* __restrict__ vlen) {
+    constexpr uint32_t U = 16 / sizeof(Sym);
+    const uint64_t upc = lpad / U;  // units per chunk
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nchunks * upc) return;
+    const uint64_t c = i / upc, k0 = (i % upc) * U;
+    const uint64_t a = span.start(c), l = span.len(c);
+    if (k0 == 0) vlen[c] = static_cast<uint32_t>(l);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+        const uint32_t v = k0 + j < l ? static_cast<uint32_t>(src[a + k0 + j]) : 0u;
+        w[j / (4 / sizeof(Sym))] |= v << (8 * sizeof(Sym) * (j % (4 / sizeof(Sym))));
+    }
+    reinterpret_cast<uint4*>(stage)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <typename Sym>
+__global__ __launch_bounds__(kBlock) void k_unstage(const Sym* __restrict__ stage, ChunkSpan<Sym> span,
+                                                    uint64_t nchunks, uint64_t lpad, Sym* __restrict__ out) {
+    constexpr uint32_t U = 16 / sizeof(Sym);
+    const uint64_t upc = lpad / U;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nchunks * upc) return;
+    const uint64_t c = i / upc, k0 = (i % upc) * U;
+    const uint64_t a = span.start(c), l = span.len(c);
+    if (k0 >= l) return;
+    const uint4 v = reinterpret_cast<const uint4*>(stage)[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+        if (k0 + j < l) {
+            const uint32_t x = w[j / (4 / sizeof(Sym))] >> (8 * sizeof(Sym) * (j % (4 / sizeof(Sym))));
+            out[a + k0 + j] = static_cast<Sym>(x);
+        }
+    }
+}
+
+template <typename Sym>
+__global__ __launch_bounds__(kBlock) void k_span_lens(ChunkSpan<Sym> span, uint64_t nchunks, uint32_t* __restrict__ vlen) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (c < nchunks) vlen[c] = static_cast<uint32_t>(span.len(c));
+}
+
+constexpr int kNotStaged = -2;
+
+// The staged route applies to the large-alphabet fast kernels (u16 / u32 symbols).
+template <typename Sym>
+bool staged_encode_ok(const ans_gpu_table* gt) {
+    return sizeof(Sym) > 1 && gt->ft.usable && gt->ft.enc_wide;
+}
+template <typename Sym>
+bool staged_decode_ok(const ans_gpu_table* gt) {
+    return sizeof(Sym) > 1 && gt->ft.usable && gt->ft.dec_wide;
+}
+
+template <typename Sym>
+int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span, uint64_t nchunks, uint64_t lmax,
+                         uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s,
+                         fast::ChunkInit ini) {
+    if constexpr (sizeof(Sym) == 1) {
+        return kNotStaged;
+    } else {
+        if (!staged_encode_ok<Sym>(gt) || nchunks == 0) return kNotStaged;
+        const FastTable& ft = gt->ft;
+        constexpr uint64_t GS = 128 / sizeof(Sym);
+        const uint64_t lpad = std::max<uint64_t>(GS, (lmax + GS - 1) / GS * GS);
+        void* mem = nullptr;
+        const size_t stage_b = nchunks * lpad * sizeof(Sym), vlen_o = (stage_b + 255) & ~size_t(255);
+        HIP_TRY(hipMallocAsync(&mem, vlen_o + 4 * nchunks, s));
+        Sym* stage = static_cast<Sym*>(mem);
+        uint32_t* vlen = reinterpret_cast<uint32_t*>(static_cast<char*>(mem) + vlen_o);
+        const uint64_t units = nchunks * lpad / (16 / sizeof(Sym));
+        k_stage<Sym><<<grid_for(units), kBlock, 0, s>>>(syms, span, nchunks, lpad, stage, vlen);
+        const unsigned grid = static_cast<unsigned>((nchunks + fast::kBlock - 1) / fast::kBlock);
+        const bool k32 = ft.K < (1ull << 32);
+        const size_t wlds = fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
+#define ENCV2(KM, K32, PK) fast::k_encode_w<Sym, KM, K32, PK, true><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
+#define ENCV(KM, K32) if (ft.enc_pack) ENCV2(KM, K32, true); else ENCV2(KM, K32, false)
+        switch (ft.kmax) {
+        case 1: case 2: if (k32) ENCV(2, true); else ENCV(2, false); break;
+        case 3: if (k32) ENCV(3, true); else ENCV(3, false); break;
+        default: if (k32) ENCV(4, true); else ENCV(4, false); break;
+        }
+#undef ENCV
+#undef ENCV2
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipFreeAsync(mem, s));
+        return ANS_OK;
+    }
+}
+
+template <typename Sym>
+int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                         const uint32_t* d_lens, ChunkSpan<Sym> span, uint64_t nchunks, uint64_t lmax, int gen_kind,
+                         Sym* out, uint32_t* d_status, hipStream_t s, fast::ChunkInit ini) {
+    if constexpr (sizeof(Sym) == 1) {
+        return kNotStaged;
+    } else {
+        if (!staged_decode_ok<Sym>(gt) || nchunks == 0) return kNotStaged;
+        const FastTable& ft = gt->ft;
+        constexpr uint64_t GS = 128 / sizeof(Sym);
+        const uint64_t lpad = std::max<uint64_t>(GS, (lmax + GS - 1) / GS * GS);
+        void* mem = nullptr;
+        const size_t stage_b = nchunks * lpad * sizeof(Sym), vlen_o = (stage_b + 255) & ~size_t(255);
+        HIP_TRY(hipMallocAsync(&mem, vlen_o + 4 * nchunks, s));
+        Sym* stage = static_cast<Sym*>(mem);
+        uint32_t* vlen = reinterpret_cast<uint32_t*>(static_cast<char*>(mem) + vlen_o);
+        const uint64_t units = nchunks * lpad / (16 / sizeof(Sym));
+        k_span_lens<Sym><<<grid_for(nchunks), kBlock, 0, s>>>(span, nchunks, vlen);
+        const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
+        if (ft.dec_c)
+            fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+        else
+            fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+        k_unstage<Sym><<<grid_for(units), kBlock, 0, s>>>(stage, span, nchunks, lpad, out);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipFreeAsync(mem, s));
+        return ANS_OK;
+    }
+}
+
 template <typename Sym>
 uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len, bool decode) {
     // the LDS-row encoder reads 128-B symbol groups; the decoders store 64-B symbol blocks
@@ -569,6 +708,11 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     const Sym* syms = static_cast<const Sym*>(d_syms);
+    if ((chunk_len * sizeof(Sym)) % 128 != 0 && staged_encode_ok<Sym>(gt)) {  // ragged chunks (C2)
+        const int rc = launch_staged_encode<Sym>(gt, syms, ChunkSpan<Sym>{nullptr, chunk_len, n}, nchunks, chunk_len,
+                                                 d_slots, slot_cap, d_lens, d_status, s, ini);
+        if (rc != kNotStaged) return rc;
+    }
     const uint64_t nfull = fast_chunks<Sym>(gt, n, chunk_len, false);
     if (nfull) {
         const FastTable& ft = gt->ft;
@@ -635,6 +779,11 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const DevTable& t = gt->t;
     const FastTable& ft = gt->ft;
     Sym* out = static_cast<Sym*>(d_syms);
+    if ((chunk_len * sizeof(Sym)) % 64 != 0 && staged_decode_ok<Sym>(gt)) {  // ragged chunks (C2)
+        const int rc = launch_staged_decode<Sym>(gt, d_in, d_offsets, slot_cap, d_lens, ChunkSpan<Sym>{nullptr, chunk_len, n},
+                                                 nchunks, chunk_len, gen_kind, out, d_status, s, ini);
+        if (rc != kNotStaged) return rc;
+    }
     // the fast kernels read whole aligned 128-B lines around each stream, from the slot layout
     // or a dense container alike (fast::DecChain::start)
     const bool lds_table = fast_chunks<Sym>(gt, n, chunk_len, true) > 0;
@@ -708,10 +857,15 @@ int launch_gen(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, voi
 template <typename Sym>
 int launch_encode_var(ans_gpu_table* gt, const void* d_syms, uint64_t nchunks, const uint64_t* d_starts,
                       uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s,
-                      fast::ChunkInit ini = {}) {
+                      fast::ChunkInit ini = {}, uint64_t lmax = 0) {
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     const Sym* syms = static_cast<const Sym*>(d_syms);
+    if (lmax) {  // the longest chunk known on the host: the staged fast kernels
+        const int rc = launch_staged_encode<Sym>(gt, syms, ChunkSpan<Sym>{d_starts, 0, 0}, nchunks, lmax, d_slots,
+                                                 slot_cap, d_lens, d_status, s, ini);
+        if (rc != kNotStaged) return rc;
+    }
     const unsigned grid = grid_for(nchunks);
     const size_t lds = gt->lds_bytes ? sizeof(DevSym) * (t.nsym + 1) : 0;
     if (gt->lds_bytes && t.fast)
@@ -729,10 +883,15 @@ int launch_encode_var(ans_gpu_table* gt, const void* d_syms, uint64_t nchunks, c
 template <typename Sym>
 int launch_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                       const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind, void* d_syms,
-                      uint32_t* d_status, hipStream_t s, fast::ChunkInit ini = {}) {
+                      uint32_t* d_status, hipStream_t s, fast::ChunkInit ini = {}, uint64_t lmax = 0) {
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     Sym* out = static_cast<Sym*>(d_syms);
+    if (lmax) {
+        const int rc = launch_staged_decode<Sym>(gt, d_in, d_offsets, slot_cap, d_lens, ChunkSpan<Sym>{d_starts, 0, 0},
+                                                 nchunks, lmax, gen_kind, out, d_status, s, ini);
+        if (rc != kNotStaged) return rc;
+    }
     const unsigned grid = grid_for(nchunks);
     const size_t lds = gt->lds_bytes;
     if (gt->lds_bytes && t.fast)
@@ -1594,6 +1753,13 @@ int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t*
 
 }  // namespace
 
+static int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                          const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap,
+                          uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax);
+static int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                          const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
+                          uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax);
+
 // Variable-chunk encode of symbols already on the device (ans_ctx.hpp): the body of
 // ans_gpu_encode_var_chunks, also used by the graph dataset coder (ans_graph.hip).
 int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
@@ -1615,9 +1781,9 @@ int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_by
     HIP_TRY(d_status.alloc(4));
     HIP_TRY(hipMemcpyAsync(d_starts.p, starts, 8 * (nchunks + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
-    int rc = ans_dev_encode_var_chunks_ex(gt, d_syms, sym_bytes, nchunks, static_cast<uint64_t*>(d_starts.p), gen_kind,
-                                          seed, static_cast<uint8_t*>(d_slots.p), slot_cap,
-                                          static_cast<uint32_t*>(d_lens.p), static_cast<uint32_t*>(d_status.p), s);
+    int rc = dev_encode_var(gt, d_syms, sym_bytes, nchunks, static_cast<uint64_t*>(d_starts.p), gen_kind, seed,
+                            static_cast<uint8_t*>(d_slots.p), slot_cap, static_cast<uint32_t*>(d_lens.p),
+                            static_cast<uint32_t*>(d_status.p), s, maxlen);
     if (rc) return rc;
     int st = 0;
     if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
@@ -1923,9 +2089,11 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
     return ANS_OK;
 }
 
-int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
-                                 const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots,
-                                 uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+// lmax > 0 (the longest chunk, known to the host callers): the staged fast kernels where the
+// table has them (launch_staged_encode); the device API passes 0 and keeps the generic kernels
+static int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                          const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap,
+                          uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || (slot_cap & 15) || !valid_kind(gen_kind)) return ANS_E_ARG;
     if (nchunks && (!d_syms || !d_starts || !d_slots || !d_lens)) return ANS_E_ARG;
@@ -1936,10 +2104,17 @@ int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_
                                        d_status, gen_kind, seed, s);
     const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
-    case 1: return launch_encode_var<uint8_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
-    case 2: return launch_encode_var<uint16_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
-    default: return launch_encode_var<uint32_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini);
+    case 1: return launch_encode_var<uint8_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini, lmax);
+    case 2: return launch_encode_var<uint16_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini, lmax);
+    default: return launch_encode_var<uint32_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini, lmax);
     }
+}
+
+int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+                                 const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots,
+                                 uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+    return dev_encode_var(gt, d_syms, sym_bytes, nchunks, d_starts, gen_kind, seed, d_slots, slot_cap, d_lens, d_status,
+                          stream, 0);
 }
 
 int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
@@ -1949,9 +2124,9 @@ int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_byt
                                         d_lens, d_status, stream);
 }
 
-int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
-                                 const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
-                                 uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+static int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                          const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
+                          uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || !valid_kind(gen_kind)) return ANS_E_ARG;
     if (nchunks && (!d_in || !d_lens || !d_starts || !d_syms)) return ANS_E_ARG;
@@ -1963,10 +2138,17 @@ int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const u
                                        seed, d_syms, sym_bytes, d_status, s);
     const fast::ChunkInit ini{gen_kind, seed};
     switch (sym_bytes) {
-    case 1: return launch_decode_var<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
-    case 2: return launch_decode_var<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
-    default: return launch_decode_var<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini);
+    case 1: return launch_decode_var<uint8_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini, lmax);
+    case 2: return launch_decode_var<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini, lmax);
+    default: return launch_decode_var<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini, lmax);
     }
+}
+
+int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                                 const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
+                                 uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+    return dev_decode_var(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, seed, d_syms, sym_bytes,
+                          d_status, stream, 0);
 }
 
 int ans_dev_decode_var_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
@@ -2018,10 +2200,12 @@ int ans_gpu_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t 
     }
     const uint64_t n = starts[nchunks];
     if ((n && !out) || (in_len && !in)) return ANS_E_ARG;
+    uint64_t maxlen = 0;
+    for (uint64_t c = 0; c < nchunks; ++c) maxlen = std::max(maxlen, starts[c + 1] - starts[c]);
     HIP_TRY(hipSetDevice(gt->g->device));
     const hipStream_t s = gt->g->stream;
     DevBuf d_in, d_offs, d_lens, d_starts, d_out, d_status;
-    HIP_TRY(d_in.alloc(in_len + 16));
+    HIP_TRY(d_in.alloc(in_len + 128));  // the fast decoders read whole 128-B lines
     HIP_TRY(d_offs.alloc(8 * nchunks));
     HIP_TRY(d_lens.alloc(4 * nchunks));
     HIP_TRY(d_starts.alloc(8 * (nchunks + 1)));
@@ -2032,10 +2216,9 @@ int ans_gpu_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t 
     HIP_TRY(hipMemcpyAsync(d_lens.p, l32.data(), 4 * nchunks, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d_starts.p, starts, 8 * (nchunks + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
-    int rc = ans_dev_decode_var_chunks_ex(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_offs.p), 0,
-                                          static_cast<uint32_t*>(d_lens.p), nchunks,
-                                          static_cast<uint64_t*>(d_starts.p), gen_kind, seed, d_out.p, sym_bytes,
-                                          static_cast<uint32_t*>(d_status.p), s);
+    int rc = dev_decode_var(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_offs.p), 0,
+                            static_cast<uint32_t*>(d_lens.p), nchunks, static_cast<uint64_t*>(d_starts.p), gen_kind,
+                            seed, d_out.p, sym_bytes, static_cast<uint32_t*>(d_status.p), s, maxlen);
     if (rc) return rc;
     int st = 0;
     if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;

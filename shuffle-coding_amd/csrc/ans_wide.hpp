@@ -62,11 +62,14 @@ __device__ __forceinline__ double rcp_newton(uint32_t p) {
 // kPack: the LDS prefix is the packed image (FastTable::enc_pack): a row costs a ds_read2_b32
 // of two block bases and two ds_read_u16 of offsets plus ~6 VALU, for ~1.8x the prefix (67%
 // of C4's symbols instead of 37%; the rest is the L2 request each).
-template <typename Sym, int KMAX, bool kK32, bool kPack>
+// kVar: chunk c holds vlen[c] <= chunk_len symbols at the start of its chunk_len-symbol stride
+// (a staged ragged or variable-length chunk, ans_kernels.hip launch_staged): its last group is
+// partial, and it is the first one coded, so the pushes past vlen[c] are skipped there.
+template <typename Sym, int KMAX, bool kK32, bool kPack, bool kVar = false>
 __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
                                                          uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                          uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
-                                                         ChunkInit ini) {
+                                                         ChunkInit ini, const uint32_t* __restrict__ vlen = nullptr) {
     extern __shared__ __align__(16) unsigned char lds[];
     {
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideEncCum);
@@ -84,7 +87,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     constexpr int GU = 8;  // units per 128-B group
     const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
-    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
+    constexpr int GS = 128 / static_cast<int>(sizeof(Sym));  // symbols per group
+    const uint32_t nvalid = kVar ? vlen[c] : static_cast<uint32_t>(chunk_len);
+    const int ngroups = kVar ? static_cast<int>((nvalid + GS - 1) / GS) : static_cast<int>(chunk_len * sizeof(Sym) / 128);
     uint8_t* dst = slots + c * slot_cap;
     const uint32_t npages_cap = static_cast<uint32_t>(slot_cap / 64);
     const uint64_t K = t.K;
@@ -144,9 +149,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 8u : 0u;
         return k;
     };
-    auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf) __attribute__((always_inline)) {
+    auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, uint32_t upos) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
+            if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
             const uint32_t sj = umin(sym_of<Sym>(unit, j), nsym);
             const bool in_lds = sj < nl;
             const v2u32 row = in_lds ? lrow(lbuf[j], sj) : gbuf[j];
@@ -169,7 +175,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     };
 
     uint4 n[GU];
-    {
+#pragma unroll
+    for (int i = 0; i < GU; ++i) n[i] = make_uint4(0, 0, 0, 0);
+    if (ngroups > 0) {  // (an empty staged chunk codes no symbol)
         const uint4* gsrc = src + GU * (ngroups - 1);
 #pragma unroll
         for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
@@ -197,7 +205,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
                 for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
             }
             if (u == 0) request(n[GU - 1], la, ga);  // unit GU-1 of group g-1 (landed units ago)
-            process(cc[u], odd ? la : lb, odd ? ga : gb);
+            process(cc[u], odd ? la : lb, odd ? ga : gb, static_cast<uint32_t>(g * GS + u * U));
         }
     }
     wait_vm();
@@ -216,7 +224,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     if (!over) pout.finish(fp, dst);
     if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
         uint32_t sym_err = 0;
-        for (uint64_t k = 0; k < chunk_len; ++k)
+        for (uint64_t k = 0; k < nvalid; ++k)
             sym_err |= static_cast<uint32_t>(syms[c * chunk_len + k]) >= t.nsym ? 1u : 0u;
         atomicOr(status, 1u << (sym_err ? ANS_E_SYMBOL : ANS_E_ZERO_MASS));
     }
@@ -353,13 +361,15 @@ struct DecChainW {
 // kPrefix: resolve cf below dec_w_cpre from the LDS prefix, else every lookup is global (the
 // compact tables: a wave step waits on L2 as soon as one of its 64 lanes misses the prefix,
 // which for C4 is nearly every step, so the prefix only added VALU to the chain).
-template <typename Sym, bool kCompact, bool kPrefix>
+// kVar: chunk c decodes vlen[c] <= chunk_len symbols into the start of its chunk_len-symbol
+// stride (staged output: the rest of its last 128-B line is garbage).
+template <typename Sym, bool kCompact, bool kPrefix, bool kVar = false>
 __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
                                                          uint64_t slot_cap, const uint64_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ lens,
                                                          uint64_t chunk_len, uint64_t nfull, int gen_kind,
                                                          Sym* __restrict__ out, uint32_t* __restrict__ status,
-                                                         ChunkInit ini) {
+                                                         ChunkInit ini, const uint32_t* __restrict__ vlen = nullptr) {
     extern __shared__ __align__(16) unsigned char lds[];
     if (kPrefix) {  // the prefix tables: bucket s0 values (u16), then cdf(0 .. nlp + 5)
         const uint32_t* gs = reinterpret_cast<const uint32_t*>(t.dec_w_s0);
@@ -378,7 +388,9 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     constexpr int UPT = 16 / U;  // units per point: 16 symbols, at most 64 stream bytes
-    const int nunit = static_cast<int>(chunk_len / U);  // a multiple of 4 (chunk bytes % 64 == 0)
+    const uint32_t nvalid = kVar ? vlen[c] : static_cast<uint32_t>(chunk_len);
+    // a multiple of 4 (chunk bytes % 64 == 0), or for kVar the units holding the chunk
+    const int nunit = static_cast<int>((nvalid + U - 1) / U);
     const uint64_t L = t.L;
     const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
@@ -494,6 +506,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
 #pragma unroll
                 for (int j = 0; j < U; ++j) {
                     __builtin_amdgcn_sched_barrier(0);
+                    if (kVar && static_cast<uint32_t>((u0 + u) * U + j) >= nvalid) continue;  // past the chunk
                     put_sym<Sym>(outv, j, step());
                 }
                 q[u] = outv;
@@ -502,8 +515,8 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
     }
     wait_vm();
     if (nunit > 0) {
-        const int rem = ((nunit - 1) & 7) + 1;  // 4 or 8
-        uint4* d = dst + (nunit - rem);
+        const int rem = kVar ? 8 : ((nunit - 1) & 7) + 1;  // 4 or 8 (staged: the whole line)
+        uint4* d = dst + ((nunit - 1) & ~7);
         if (rem == 8) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) d[k] = q[k];

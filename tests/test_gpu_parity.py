@@ -634,13 +634,14 @@ def test_rare_rows_whole_waves(gpu):
 
 
 # ---------------------------------------------------------------- variable-length chunks
-@pytest.mark.parametrize("which", ["c3", "multiset", "tiny_norm"])
+@pytest.mark.parametrize("which", ["c3", "multiset", "tiny_norm", "c4"])
 def test_var_chunks_bit_exact(gpu, which, multiset_masses):
     """Chunk c = syms[starts[c]:starts[c+1]] (empty, one-symbol and long chunks mixed): each
-    stream is the reference message of that slice alone (one oracle message per chunk)."""
+    stream is the reference message of that slice alone (one oracle message per chunk).
+    The large-alphabet tables (multiset: 1,024 symbols; c4) take the staged fast kernels."""
     rng = np.random.default_rng(31)
     masses = {"c3": A.c3_masses(), "multiset": multiset_masses,
-              "tiny_norm": np.asarray([3, 0, 5, 1, 7], np.uint64)}[which]
+              "tiny_norm": np.asarray([3, 0, 5, 1, 7], np.uint64), "c4": A.c4_masses()}[which]
     sizes = np.concatenate([[0, 1, 0, 7], rng.integers(0, 3000, 300), [20000, 0]]).astype(np.uint64)
     starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
     n = int(starts[-1])
@@ -695,6 +696,36 @@ def test_wide_kernels_bit_exact(gpu, nsym, lo, hi, ones, zeros, crowd, chunk_len
     syms = np.where(rng.random(n) < 0.5, rng.choice(nz, size=n, p=p / p.sum()), rng.choice(nz, size=n))
     for dtype in (np.uint16, np.uint32):
         _roundtrip_vs_oracle(gpu, masses, syms.astype(np.uint32), chunk_len, dtype)
+
+
+@pytest.mark.parametrize("chunk_len,n", [(1563, 300 * 1563 + 77), (1, 500), (63, 64 * 63), (4100, 70 * 4100)])
+def test_staged_ragged_chunks_bit_exact(gpu, chunk_len, n):
+    """Chunk lengths whose bytes are no multiple of the fast kernels' 128-B groups (C2's 1,563
+    u16 symbols) take the staged large-alphabet kernels (k_encode_w / k_decode_w with kVar),
+    dense and slot layouts alike."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(chunk_len)
+    masses = A.c4_masses()
+    syms = rng.integers(0, 65536, size=n).astype(np.uint16)
+    _roundtrip_vs_oracle(gpu, masses, syms.astype(np.uint32), chunk_len, np.uint16)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    try:
+        nch = -(-n // chunk_len)
+        cap = gt.slot_capacity(chunk_len)
+        d_syms = torch.from_numpy(syms.view(np.int16)).cuda()
+        slots = torch.empty(nch * cap, dtype=torch.uint8, device="cuda")
+        lens = torch.zeros(nch, dtype=torch.int32, device="cuda")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        gt.dev_encode(d_syms, 2, n, chunk_len, slots, cap, lens, status, stream)
+        out = torch.empty_like(d_syms)
+        gt.dev_decode(slots, None, cap, lens, n, chunk_len, out, 2, status, stream)
+        assert gpu.status(status, stream) == 0
+        assert torch.equal(out, d_syms)
+    finally:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(torch.cuda.default_stream())
 
 
 def test_wide_kernel_errors(gpu):
