@@ -95,3 +95,12 @@ int ans_tableset_host_encode(struct ans_gpu_tableset* ts, const void* syms, int 
 int ans_tableset_host_decode(struct ans_gpu_tableset* ts, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                              const uint64_t* lens, uint64_t n, uint64_t chunk_len, const uint64_t* starts,
                              uint64_t nchunks, int gen_kind, uint64_t seed, void* out, int w);
+
+// Variable-length chunks with the longest chunk's length known to the caller (lmax > 0): the
+// staged fast kernels where the table has them (ans_kernels.hip launch_staged_*), else generic.
+extern "C" __attribute__((visibility("hidden"))) int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks, const uint64_t* d_starts,
+                   int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
+                   uint32_t* d_status, void* stream, uint64_t lmax);
+extern "C" __attribute__((visibility("hidden"))) int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+                   const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind, uint64_t seed,
+                   void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax);

@@ -281,12 +281,17 @@ struct PageOut {
 // probability 1e-5).  Every row then reads KMAX - 1 thresholds; those rare rows carry a negative
 // rcp and add the last threshold's test on a wave-voted branch (one 8-byte LDS read, one
 // 64-bit compare and one add fewer per symbol).
-template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kRare = false>
+// kVar (LDS rows only): chunk c holds vlen[c] <= chunk_len symbols at the start of its stride
+// (staged ragged / variable-length chunks, ans_kernels.hip launch_staged_encode); the pushes
+// past vlen[c], all in its first-coded group, are skipped.
+template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kRare = false, bool kVar = false>
 __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTable t, const Sym* __restrict__ syms,
                                                                          uint64_t chunk_len, uint64_t nfull,
                                                                          uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                                          uint32_t* __restrict__ lens,
-                                                                         uint32_t* __restrict__ status, ChunkInit ini) {
+                                                                         uint32_t* __restrict__ status, ChunkInit ini,
+                                                                         const uint32_t* __restrict__ vlen = nullptr) {
+    static_assert(!(kVar && kGlobalRows), "staged chunks take the LDS-row kernel");
     extern __shared__ __align__(16) unsigned char lds[];
     // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
     // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
@@ -396,7 +401,8 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb)), "s"(static_cast<uint32_t>(norm)));
         head = mk64(hi32(lo64) + hq - exp_norm, lo32(lo64));
     };
-    auto process = [&](const uint4& unit) __attribute__((always_inline)) {
+    const uint32_t nvalid = kVar ? vlen[c] : static_cast<uint32_t>(chunk_len);
+    auto process = [&](const uint4& unit, uint32_t upos) __attribute__((always_inline)) {
         // rows are read one symbol ahead; the scheduling barriers keep the compiler from
         // hoisting all sixteen reads (and their registers) to the top of the unit
         auto rsym = [&](int j) __attribute__((always_inline)) {
@@ -408,6 +414,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             __builtin_amdgcn_sched_barrier(0);
             const Row e = e_next;
             if (j > 0) e_next = row(rsym(j - 1));
+            if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
             uint32_t k8 = bytes_out_thr8(e.thr);
             if constexpr (kRare) {
                 EncRow r = e.e;
@@ -479,9 +486,12 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         // and stays in flight for four units; no explicit wait: the page stores need none (their
         // data leaves the registers at issue), and the compiler waits for the loads at first use.
         constexpr int GU = 8;
-        const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
+        constexpr int GS = 128 / static_cast<int>(sizeof(Sym));  // symbols per group
+        const int ngroups = kVar ? static_cast<int>((nvalid + GS - 1) / GS) : static_cast<int>(chunk_len * sizeof(Sym) / 128);
         uint4 n[GU];
-        {
+#pragma unroll
+        for (int i = 0; i < GU; ++i) n[i] = make_uint4(0, 0, 0, 0);
+        if (ngroups > 0) {  // (an empty staged chunk codes no symbol)
             const uint4* gsrc = src + GU * (ngroups - 1);
 #pragma unroll
             for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
@@ -505,7 +515,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 #pragma unroll
                     for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
                 }
-                process(cc[u]);
+                process(cc[u], static_cast<uint32_t>(g * GS + u * U));
             }
         }
     }
@@ -525,7 +535,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     if (!over) pout.finish(fp, dst);
     if (minmass == 0) {  // classify like the reference: out-of-range index (codec.rs:63) or p == 0 (ans.rs:98)
         uint32_t sym_err = 0;
-        for (uint64_t k = 0; k < chunk_len; ++k)
+        for (uint64_t k = 0; k < nvalid; ++k)
             sym_err |= static_cast<uint32_t>(syms[c * chunk_len + k]) >= t.nsym ? 1u : 0u;
         atomicOr(status, 1u << (sym_err ? ANS_E_SYMBOL : ANS_E_ZERO_MASS));
     }
@@ -808,12 +818,14 @@ struct DecChain {
 // SPP: symbols per point (U, or U/2 when U*KMAX > 60: u8 tables whose pops can take 4 bytes).
 // kFar: some bucket holds more than four cdf boundaries, so the voted slow path is compiled in.
 // kP24: every mass is below 2^24 (DecChain::update).  kJ4: some pop can pull 4 bytes (kmax = 4).
-template <typename Sym, int SPP, bool kFar, bool kP24, bool kJ4>
+// kVar: chunk c decodes vlen[c] <= chunk_len symbols into the start of its stride (staged output).
+template <typename Sym, int SPP, bool kFar, bool kP24, bool kJ4, bool kVar = false>
 __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint64_t* __restrict__ offsets,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
                                                       uint64_t nfull, int gen_kind, Sym* __restrict__ out,
-                                                      uint32_t* __restrict__ status, ChunkInit ini) {
+                                                      uint32_t* __restrict__ status, ChunkInit ini,
+                                                      const uint32_t* __restrict__ vlen = nullptr) {
     extern __shared__ __align__(16) unsigned char lds[];
     unsigned char* tab = lds;  // tables at offset 0, ring after them
     {
@@ -830,7 +842,8 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
     static_assert(U % SPP == 0, "points must split units evenly");
-    const int nunit = static_cast<int>(chunk_len / U);
+    const uint32_t nvalid = kVar ? vlen[c] : static_cast<uint32_t>(chunk_len);
+    const int nunit = static_cast<int>((nvalid + U - 1) / U);
     const uint64_t L = t.L;
     const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
@@ -868,6 +881,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                 ch.point();
             }
             __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
+            if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
             ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
             if constexpr (kFar) {
                 ch.lookup(shift);
@@ -890,9 +904,9 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
         }
     }
     wait_vm();
-    if (nunit > 0) {  // the last (partial) line: 4 or 8 units (chunk bytes % 64 == 0)
-        const int rem = ((nunit - 1) & 7) + 1;
-        uint4* d = dst + (nunit - rem);
+    if (nunit > 0) {  // the last (partial) line: 4 or 8 units (chunk bytes % 64 == 0; staged: all 8)
+        const int rem = kVar ? 8 : ((nunit - 1) & 7) + 1;
+        uint4* d = dst + ((nunit - 1) & ~7);
         if (rem == 8) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) d[k] = q[k];

@@ -547,7 +547,7 @@ int ans_gpu_dense_sets_decode(ans_gpu_table* gt, uint64_t num_graphs, const uint
     const hipStream_t s = gp->stream;
     const uint64_t ntiles = (len + kTileSlots - 1) / kTileSlots;
     Buf d_in, d_offs, d_lens, d_S, d_nn, d_dense, d_status, d_edges, d_scan, d_eo;
-    if (!d_in.alloc(in_len + 16) || !d_offs.alloc(8 * num_graphs) || !d_lens.alloc(4 * num_graphs) ||
+    if (!d_in.alloc(in_len + 128) || !d_offs.alloc(8 * num_graphs) || !d_lens.alloc(4 * num_graphs) ||
         !d_S.alloc(8 * (num_graphs + 1)) || !d_nn.alloc(4 * num_graphs) || !d_dense.alloc(len + 16) ||
         !d_status.alloc(16) || !d_edges.alloc(8 * cap) || !d_scan.alloc(12 * ntiles + 16) ||
         !d_eo.alloc(8 * (num_graphs + 1)))
@@ -558,9 +558,10 @@ int ans_gpu_dense_sets_decode(ans_gpu_table* gt, uint64_t num_graphs, const uint
     HIP_TRY(hipMemcpyAsync(d_S.p, S.data(), 8 * (num_graphs + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d_nn.p, num_nodes, 4 * num_graphs, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 16, s));
-    int rc = ans_dev_decode_var_chunks(gt, d_in.as<uint8_t>(), d_offs.as<uint64_t>(), 0, d_lens.as<uint32_t>(),
-                                       num_graphs, d_S.as<uint64_t>(), ANS_GEN_ZEROS, d_dense.p, 1,
-                                       d_status.as<uint32_t>(), s);
+    uint64_t maxlen = 0;  // the longest graph's slot count: the staged fast decoder (ans_ctx.hpp)
+    for (uint64_t g = 0; g < num_graphs; ++g) maxlen = std::max(maxlen, S[g + 1] - S[g]);
+    int rc = dev_decode_var(gt, d_in.as<uint8_t>(), d_offs.as<uint64_t>(), 0, d_lens.as<uint32_t>(), num_graphs,
+                            d_S.as<uint64_t>(), ANS_GEN_ZEROS, 0, d_dense.p, 1, d_status.as<uint32_t>(), s, maxlen);
     if (rc) return rc;
     auto* base = d_scan.as<uint64_t>();
     auto* counts = reinterpret_cast<uint32_t*>(base + ntiles);

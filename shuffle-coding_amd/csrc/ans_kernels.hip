@@ -618,21 +618,19 @@ constexpr int kNotStaged = -2;
 
 // The staged route applies to the large-alphabet fast kernels (u16 / u32 symbols).
 template <typename Sym>
-bool staged_encode_ok(const ans_gpu_table* gt) {
-    return sizeof(Sym) > 1 && gt->ft.usable && gt->ft.enc_wide;
+bool staged_encode_ok(const ans_gpu_table* gt) {  // large-alphabet or LDS-row encoder
+    return gt->ft.usable && ((sizeof(Sym) > 1 && gt->ft.enc_wide) || !gt->ft.enc_global);
 }
 template <typename Sym>
-bool staged_decode_ok(const ans_gpu_table* gt) {
-    return sizeof(Sym) > 1 && gt->ft.usable && gt->ft.dec_wide;
+bool staged_decode_ok(const ans_gpu_table* gt) {  // large-alphabet or LDS-bucket decoder
+    return gt->ft.usable && ((sizeof(Sym) > 1 && gt->ft.dec_wide) || gt->ft.dec_usable);
 }
 
 template <typename Sym>
 int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span, uint64_t nchunks, uint64_t lmax,
                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s,
                          fast::ChunkInit ini) {
-    if constexpr (sizeof(Sym) == 1) {
-        return kNotStaged;
-    } else {
+    {
         if (!staged_encode_ok<Sym>(gt) || nchunks == 0) return kNotStaged;
         const FastTable& ft = gt->ft;
         constexpr uint64_t GS = 128 / sizeof(Sym);
@@ -647,15 +645,28 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
         const unsigned grid = static_cast<unsigned>((nchunks + fast::kBlock - 1) / fast::kBlock);
         const bool k32 = ft.K < (1ull << 32);
         const size_t wlds = fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
+        if (sizeof(Sym) > 1 && ft.enc_wide) {
 #define ENCV2(KM, K32, PK) fast::k_encode_w<Sym, KM, K32, PK, true><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
 #define ENCV(KM, K32) if (ft.enc_pack) ENCV2(KM, K32, true); else ENCV2(KM, K32, false)
-        switch (ft.kmax) {
-        case 1: case 2: if (k32) ENCV(2, true); else ENCV(2, false); break;
-        case 3: if (k32) ENCV(3, true); else ENCV(3, false); break;
-        default: if (k32) ENCV(4, true); else ENCV(4, false); break;
-        }
+            switch (ft.kmax) {
+            case 1: case 2: if (k32) ENCV(2, true); else ENCV(2, false); break;
+            case 3: if (k32) ENCV(3, true); else ENCV(3, false); break;
+            default: if (k32) ENCV(4, true); else ENCV(4, false); break;
+            }
 #undef ENCV
 #undef ENCV2
+        } else {  // LDS rows (ans_fast.hpp k_encode, kVar)
+#define ENCL(KM, K32, R) fast::k_encode<Sym, KM, K32, false, R, true><<<grid, fast::kBlock, fast::kEncSharedBytes, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
+#define ENCL_R(KM, K32) if (ft.enc_rare) ENCL(KM, K32, true); else ENCL(KM, K32, false)
+            switch (ft.kmax) {
+            case 1: if (k32) ENCL(2, true, false); else ENCL(2, false, false); break;
+            case 2: if (k32) ENCL_R(2, true); else ENCL_R(2, false); break;
+            case 3: if (k32) ENCL_R(3, true); else ENCL_R(3, false); break;
+            default: if (k32) ENCL_R(4, true); else ENCL_R(4, false); break;
+            }
+#undef ENCL_R
+#undef ENCL
+        }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipFreeAsync(mem, s));
         return ANS_OK;
@@ -666,9 +677,7 @@ template <typename Sym>
 int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                          const uint32_t* d_lens, ChunkSpan<Sym> span, uint64_t nchunks, uint64_t lmax, int gen_kind,
                          Sym* out, uint32_t* d_status, hipStream_t s, fast::ChunkInit ini) {
-    if constexpr (sizeof(Sym) == 1) {
-        return kNotStaged;
-    } else {
+    {
         if (!staged_decode_ok<Sym>(gt) || nchunks == 0) return kNotStaged;
         const FastTable& ft = gt->ft;
         constexpr uint64_t GS = 128 / sizeof(Sym);
@@ -680,11 +689,28 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
         uint32_t* vlen = reinterpret_cast<uint32_t*>(static_cast<char*>(mem) + vlen_o);
         const uint64_t units = nchunks * lpad / (16 / sizeof(Sym));
         k_span_lens<Sym><<<grid_for(nchunks), kBlock, 0, s>>>(span, nchunks, vlen);
-        const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
-        if (ft.dec_c)
-            fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
-        else
-            fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+        if (sizeof(Sym) > 1 && ft.dec_wide) {
+            const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
+            if (ft.dec_c)
+                fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+            else
+                fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+        } else {  // LDS buckets (ans_fast.hpp k_decode, kVar)
+            const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
+            const unsigned dgrid = static_cast<unsigned>((nchunks + fast::kDecBlock - 1) / fast::kDecBlock);
+            constexpr int U = 16 / sizeof(Sym);
+#define DECV(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4, true><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
+#define DECV_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DECV(SPP, FAR, true, J4); else DECV(SPP, FAR, false, J4)
+#define DECV_J(SPP, FAR) if (ft.kmax >= 4) { DECV_P(SPP, FAR, true); } else { DECV_P(SPP, FAR, false); }
+            if (U * ft.kmax > 60) {
+                if (ft.dec_far) { DECV_P(U / 2, true, true); } else { DECV_P(U / 2, false, true); }
+            } else {
+                if (ft.dec_far) { DECV_J(U, true); } else { DECV_J(U, false); }
+            }
+#undef DECV_J
+#undef DECV_P
+#undef DECV
+        }
         k_unstage<Sym><<<grid_for(units), kBlock, 0, s>>>(stage, span, nchunks, lpad, out);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipFreeAsync(mem, s));
@@ -1753,13 +1779,6 @@ int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t*
 
 }  // namespace
 
-static int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
-                          const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap,
-                          uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax);
-static int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
-                          const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
-                          uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax);
-
 // Variable-chunk encode of symbols already on the device (ans_ctx.hpp): the body of
 // ans_gpu_encode_var_chunks, also used by the graph dataset coder (ans_graph.hip).
 int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
@@ -2091,7 +2110,7 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
 
 // lmax > 0 (the longest chunk, known to the host callers): the staged fast kernels where the
 // table has them (launch_staged_encode); the device API passes 0 and keeps the generic kernels
-static int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
+int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                           const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap,
                           uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
@@ -2124,7 +2143,7 @@ int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_byt
                                         d_lens, d_status, stream);
 }
 
-static int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
+int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                           const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
                           uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax) {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread

@@ -698,16 +698,23 @@ def test_wide_kernels_bit_exact(gpu, nsym, lo, hi, ones, zeros, crowd, chunk_len
         _roundtrip_vs_oracle(gpu, masses, syms.astype(np.uint32), chunk_len, dtype)
 
 
-@pytest.mark.parametrize("chunk_len,n", [(1563, 300 * 1563 + 77), (1, 500), (63, 64 * 63), (4100, 70 * 4100)])
-def test_staged_ragged_chunks_bit_exact(gpu, chunk_len, n):
+@pytest.mark.parametrize("table,chunk_len,n", [("c4", 1563, 300 * 1563 + 77), ("c4", 1, 500), ("c4", 63, 64 * 63),
+                                               ("c4", 4100, 70 * 4100), ("c3", 1000, 600 * 1000 + 5),
+                                               ("c3", 7, 3000), ("bernoulli", 333, 2000 * 333)])
+def test_staged_ragged_chunks_bit_exact(gpu, table, chunk_len, n):
     """Chunk lengths whose bytes are no multiple of the fast kernels' 128-B groups (C2's 1,563
-    u16 symbols) take the staged large-alphabet kernels (k_encode_w / k_decode_w with kVar),
-    dense and slot layouts alike."""
+    u16 symbols) take the staged kernels (k_encode_w / k_decode_w, or the LDS-row k_encode /
+    k_decode, with kVar), dense and slot layouts alike."""
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(chunk_len)
-    masses = A.c4_masses()
-    syms = rng.integers(0, 65536, size=n).astype(np.uint16)
+    masses = {"c4": A.c4_masses(), "c3": A.c3_masses(),
+              "bernoulli": np.asarray([(1 << 28) - 26843, 26843], np.uint64)}[table]
+    nz = np.flatnonzero(masses)
+    p = masses[nz].astype(np.float64)
+    syms = rng.choice(nz, size=n, p=p / p.sum()).astype(np.uint16)
     _roundtrip_vs_oracle(gpu, masses, syms.astype(np.uint32), chunk_len, np.uint16)
+    if len(masses) <= 256:
+        _roundtrip_vs_oracle(gpu, masses, syms.astype(np.uint32), chunk_len, np.uint8)
     gt = A.GpuTable(gpu, A.Categorical(masses))
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
