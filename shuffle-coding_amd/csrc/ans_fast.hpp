@@ -1127,5 +1127,72 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
     else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }
 
+// ====================================================================== bulk sampling
+// Codec::samples (src/ans.rs:38-44) on the fast decoder's tables: chunk c = len pops from
+// Message::random(seed + c) (head 1 then renorm_up from the generator, src/ans.rs:285-290),
+// every renorm byte drawn from TailGenerator::Random (src/ans.rs:142-157).  The decode
+// buckets and cdf sit in LDS as in k_decode (one 1,024-lane workgroup per CU shares them);
+// q, cf by the f64 estimate (div_norm), the icdf by the 3-candidate bucket plus the voted
+// scan, head = p*q + cf - cum.  Symbols leave in 16-B groups per lane when the chunk is
+// aligned, else one by one.
+template <typename Sym>
+__global__ __launch_bounds__(kDecBlock, 4) void k_sample(FastTable t, uint64_t seed, uint64_t n, uint64_t chunk_len,
+                                                      uint64_t nchunks, Sym* __restrict__ out) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    {
+        uint4* b = reinterpret_cast<uint4*>(lds);
+        const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt);
+        for (uint32_t i = threadIdx.x; i < t.dec_cum_off / 16; i += kDecBlock) b[i] = gb[i];
+        uint32_t* cl = reinterpret_cast<uint32_t*>(lds + t.dec_cum_off);
+        for (uint32_t i = threadIdx.x; i < t.nsym + 5; i += kDecBlock) cl[i] = t.cum[i];
+    }
+    const uint32_t* lcum = reinterpret_cast<const uint32_t*>(lds + t.dec_cum_off);
+    __syncthreads();
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kDecBlock + threadIdx.x;
+    if (c >= nchunks) return;
+    Pcg64Mcg rng;
+    rng.seed_from_u64(seed + c);
+    uint64_t head = 1;
+    while (head < kMaxMinHead) head = (head << 8) | rng.next_byte();
+    const uint64_t L = t.L;
+    const uint32_t norm = t.norm, shift = t.dec_shift;
+    const double rcp_norm = t.rcp_norm;
+    auto pop = [&]() __attribute__((always_inline)) {
+        while (head < L) head = (head << 8) | rng.next_byte();  // renorm (src/ans.rs:109,239-243)
+        uint64_t qq;
+        uint32_t cf;
+        div_norm(head, norm, rcp_norm, qq, cf);
+        const uint32_t bi = cf >> shift;
+        const uint64_t ca = lds_ld64(bi << 3), cb = lds_ld64((bi << 3) + 8 * kDecNbMax);
+        const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0Off));
+        const bool b1 = cf >= hi32(ca), b2 = cf >= lo32(cb);
+        uint32_t cum = b2 ? lo32(cb) : (b1 ? hi32(ca) : lo32(ca));
+        uint32_t nxt = b2 ? hi32(cb) : (b1 ? lo32(cb) : hi32(ca));
+        uint32_t sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u);
+        if (__builtin_expect(__any(cf >= hi32(cb)), 0)) {
+            if (cf >= hi32(cb)) {  // 3+ boundaries in the bucket: scan the staged cdf
+                sx += 1;
+                while (cf >= lcum[sx + 1]) ++sx;
+                cum = lcum[sx];
+                nxt = lcum[sx + 1];
+            }
+        }
+        head = qq * (nxt - cum) + (cf - cum);  // src/ans.rs:113-114
+        return sx;
+    };
+    const uint64_t a = c * chunk_len, b = min(a + chunk_len, n);
+    uint64_t k = a;
+    constexpr int U = 16 / static_cast<int>(sizeof(Sym));
+    if ((a * sizeof(Sym)) % 16 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+        for (; k + U <= b; k += U) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < U; ++j) put_sym<Sym>(v, j, pop());
+            *reinterpret_cast<uint4*>(out + k) = v;
+        }
+    }
+    for (; k < b; ++k) out[k] = static_cast<Sym>(pop());
+}
+
 }  // namespace fast
 }  // namespace shuffle_coding

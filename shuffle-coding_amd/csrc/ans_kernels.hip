@@ -936,8 +936,14 @@ template <typename Sym>
 int launch_sample(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* d_syms, hipStream_t s) {
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks == 0) return ANS_OK;
-    const unsigned grid = grid_for(nchunks);
     Sym* out = static_cast<Sym*>(d_syms);
+    if (gt->ft.usable && gt->ft.dec_usable) {  // the fast decoder's LDS tables (ans_fast.hpp k_sample)
+        const unsigned dgrid = static_cast<unsigned>((nchunks + fast::kDecBlock - 1) / fast::kDecBlock);
+        fast::k_sample<Sym><<<dgrid, fast::kDecBlock, gt->ft.dec_lds_bytes, s>>>(gt->ft, seed, n, chunk_len, nchunks, out);
+        HIP_TRY(hipGetLastError());
+        return ANS_OK;
+    }
+    const unsigned grid = grid_for(nchunks);
     if (gt->lds_bytes && gt->t.fast)
         k_sample_iid<Sym, true, true><<<grid, kBlock, gt->lds_bytes, s>>>(gt->t, seed, n, chunk_len, nchunks, out);
     else if (gt->lds_bytes)
