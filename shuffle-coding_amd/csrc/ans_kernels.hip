@@ -667,8 +667,9 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
 #undef ENCL_R
 #undef ENCL
         }
-        HIP_TRY(hipGetLastError());
+        const hipError_t err = hipGetLastError();  // free the staging buffer on every path
         HIP_TRY(hipFreeAsync(mem, s));
+        HIP_TRY(err);
         return ANS_OK;
     }
 }
@@ -712,8 +713,9 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
 #undef DECV
         }
         k_unstage<Sym><<<grid_for(units), kBlock, 0, s>>>(stage, span, nchunks, lpad, out);
-        HIP_TRY(hipGetLastError());
+        const hipError_t err = hipGetLastError();  // free the staging buffer on every path
         HIP_TRY(hipFreeAsync(mem, s));
+        HIP_TRY(err);
         return ANS_OK;
     }
 }
