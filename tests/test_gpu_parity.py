@@ -783,17 +783,60 @@ def test_random_message_multiset_fixtures(gpu, size, chunks, multiset_masses, mu
         _roundtrip_random(gpu, multiset_masses, syms, chunk_len, dtype, 0)
 
 
-@pytest.mark.parametrize("which", ["c3", "c4", "bernoulli"])
+@pytest.mark.parametrize("which", ["c3", "c4", "bernoulli", "c4_staged", "c3_staged"])
 def test_random_message_fast_kernels(gpu, which):
-    """Message::random(seed + c) on the fast kernels (LDS rows / wide tables), against the oracle."""
+    """Message::random(seed + c) on the fast kernels (LDS rows / wide tables, and their staged
+    ragged-chunk forms), against the oracle."""
+    chunk_len = 4096
     if which == "c3":
         masses, n, dtype = A.c3_masses(), 1100 * 4096 + 5, np.uint8
     elif which == "c4":
         masses, n, dtype = A.c4_masses(), 600 * 4096, np.uint16
+    elif which == "c4_staged":
+        masses, n, dtype, chunk_len = A.c4_masses(), 300 * 1563 + 11, np.uint16, 1563
+    elif which == "c3_staged":
+        masses, n, dtype, chunk_len = A.c3_masses(), 500 * 1000 + 3, np.uint8, 1000
     else:
         masses, n, dtype = np.array([(1 << 28) - 26843, 26843], np.uint64), 700 * 4096, np.uint8
     syms = orc.gen_iid(masses, 9, 0, n)
-    _roundtrip_random(gpu, masses, syms, 4096, dtype, 12345)
+    _roundtrip_random(gpu, masses, syms, chunk_len, dtype, 12345)
+
+
+@pytest.mark.parametrize("which", ["c3", "c4"])
+def test_random_message_dense_container(gpu, which):
+    """ans_dev_encode_dense_ex from Message::random(seed + c): the packed bytes equal the
+    oracle's, and decoding the container in place returns the symbols."""
+    torch = pytest.importorskip("torch")
+    masses, n, sb = (A.c3_masses(), 300 * 4096, 1) if which == "c3" else (A.c4_masses(), 200 * 4096, 2)
+    seed, L = 4242, 4096
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    try:
+        nch = n // L
+        cap = gt.slot_capacity(L)
+        syms = torch.empty(n, dtype=torch.uint8 if sb == 1 else torch.int16, device="cuda")
+        gt.dev_gen_iid(5, 0, n, syms, sb, stream)
+        slots = torch.empty(nch * cap, dtype=torch.uint8, device="cuda")
+        lens = torch.zeros(nch, dtype=torch.int32, device="cuda")
+        offs = torch.empty(A.dense_offsets_entries(nch), dtype=torch.int64, device="cuda")
+        dense = torch.empty(nch * cap, dtype=torch.uint8, device="cuda")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        gt.dev_encode_dense(syms, sb, n, L, slots, cap, lens, offs, dense, status, stream,
+                            gen_kind=A.GEN_RANDOM, seed=seed)
+        out = torch.empty_like(syms)
+        gt.dev_decode(dense, offs, cap, lens, n, L, out, sb, status, stream, gen_kind=A.GEN_RANDOM, seed=seed)
+        assert gpu.status(status, stream) == 0
+        assert torch.equal(out, syms)
+        torch.cuda.synchronize()
+        total = int(offs[nch].item())
+        host = syms.cpu().numpy().view(np.uint8 if sb == 1 else np.uint16).astype(np.uint32)
+        od, _, ol = orc.encode_chunks(masses, host, L, kind=orc.RANDOM, seed=seed)
+        assert np.array_equal(lens.cpu().numpy().astype(np.int64), ol.astype(np.int64))
+        assert dense[:total].cpu().numpy().tobytes() == od.tobytes()
+    finally:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(torch.cuda.default_stream())
 
 
 def test_random_message_device_api(gpu):
