@@ -241,9 +241,9 @@ def main():
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
-    # (a short pass, so the headline kernels dominate a rocprof average of the same command)
+    # (its own warmup: clocks drop while the slot pass is verified; at most 10 timed steps)
     dense = None if args.no_dense else dense_pass(gt, syms, sym_bytes, n, L, nchunks, slots, cap, status, stream,
-                                                  min(args.steps, 5), min(args.warmup, 2))
+                                                  min(args.steps, 10), args.warmup)
     if dense is not None and (not dense.pop("ok") or gpu.status(status, stream) != 0):
         bad = 1.0
     t = torch.tensor([elapsed, bad], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
