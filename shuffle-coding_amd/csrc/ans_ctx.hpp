@@ -104,3 +104,10 @@ extern "C" __attribute__((visibility("hidden"))) int dev_encode_var(ans_gpu_tabl
 extern "C" __attribute__((visibility("hidden"))) int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                    const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind, uint64_t seed,
                    void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax);
+// lmax for dev_*_var when the staged layout (every chunk padded to the longest, rounded to
+// 128 B) stays within twice the symbols plus 64 MiB; 0 (the generic kernels) otherwise
+inline uint64_t staged_lmax(uint64_t nchunks, uint64_t maxlen, uint64_t total, int sym_bytes) {
+    const uint64_t per = ((maxlen * static_cast<uint64_t>(sym_bytes) + 127) / 128) * 128;
+    const uint64_t staged = nchunks * per, budget = 2 * total * static_cast<uint64_t>(sym_bytes) + (64ull << 20);
+    return (maxlen == 0 || staged > budget) ? 0 : maxlen;
+}

@@ -561,7 +561,8 @@ int ans_gpu_dense_sets_decode(ans_gpu_table* gt, uint64_t num_graphs, const uint
     uint64_t maxlen = 0;  // the longest graph's slot count: the staged fast decoder (ans_ctx.hpp)
     for (uint64_t g = 0; g < num_graphs; ++g) maxlen = std::max(maxlen, S[g + 1] - S[g]);
     int rc = dev_decode_var(gt, d_in.as<uint8_t>(), d_offs.as<uint64_t>(), 0, d_lens.as<uint32_t>(), num_graphs,
-                            d_S.as<uint64_t>(), ANS_GEN_ZEROS, 0, d_dense.p, 1, d_status.as<uint32_t>(), s, maxlen);
+                            d_S.as<uint64_t>(), ANS_GEN_ZEROS, 0, d_dense.p, 1, d_status.as<uint32_t>(), s,
+                            staged_lmax(num_graphs, maxlen, len, 1));
     if (rc) return rc;
     auto* base = d_scan.as<uint64_t>();
     auto* counts = reinterpret_cast<uint32_t*>(base + ntiles);

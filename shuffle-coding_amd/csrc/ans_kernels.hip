@@ -1810,7 +1810,8 @@ int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_by
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
     int rc = dev_encode_var(gt, d_syms, sym_bytes, nchunks, static_cast<uint64_t*>(d_starts.p), gen_kind, seed,
                             static_cast<uint8_t*>(d_slots.p), slot_cap, static_cast<uint32_t*>(d_lens.p),
-                            static_cast<uint32_t*>(d_status.p), s, maxlen);
+                            static_cast<uint32_t*>(d_status.p), s,
+                            staged_lmax(nchunks, maxlen, starts[nchunks] - starts[0], sym_bytes));
     if (rc) return rc;
     int st = 0;
     if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
@@ -2245,7 +2246,8 @@ int ans_gpu_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t 
     HIP_TRY(hipMemsetAsync(d_status.p, 0, 4, s));
     int rc = dev_decode_var(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_offs.p), 0,
                             static_cast<uint32_t*>(d_lens.p), nchunks, static_cast<uint64_t*>(d_starts.p), gen_kind,
-                            seed, d_out.p, sym_bytes, static_cast<uint32_t*>(d_status.p), s, maxlen);
+                            seed, d_out.p, sym_bytes, static_cast<uint32_t*>(d_status.p), s,
+                            staged_lmax(nchunks, maxlen, n, sym_bytes));
     if (rc) return rc;
     int st = 0;
     if ((rc = ans_dev_status(gt->g, static_cast<uint32_t*>(d_status.p), s, &st))) return rc;
