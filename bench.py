@@ -40,8 +40,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 CONFIGS = {
     # name: (masses fn, log2 n per rank, symbol bytes, seed)
     "c3": (A.c3_masses, 30, 1, 1),
+    "c3p2": (A.c3_pow2_masses, 30, 1, 1),  # C3's table quantised to norm 2^24
     "c4": (A.c4_masses, 29, 2, 2),
 }
+HBM_COPY_GBS = 6290.0  # measured float4 copy (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def parse():
@@ -55,6 +57,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-dense", action="store_true", help="skip the dense-container pass")
+    p.add_argument("--strong", action="store_true",
+                   help="strong scaling: the config's 2^log2n symbols in total, split over the ranks")
     return p.parse_args()
 
 
@@ -189,7 +193,15 @@ def main():
     masses_fn, log2n, sym_bytes, seed = CONFIGS[args.config]
     if args.log2n is not None:
         log2n = args.log2n
-    n = 1 << log2n
+    if args.strong:  # the 2^log2n-symbol array split into whole-chunk ranges, one per rank
+        sys.path.insert(0, os.path.join(ROOT, "shuffle-coding_amd"))
+        import shards
+        total_n = 1 << log2n
+        start, end, _, _ = shards.shard_symbols(total_n, args.chunk_len, world, rank)
+        n = end - start
+    else:
+        n = 1 << log2n
+        start, total_n = rank * n, world * n
     L = args.chunk_len
     nchunks = -(-n // L)
     masses = masses_fn()
@@ -203,7 +215,7 @@ def main():
     torch.cuda.set_stream(stream)
     dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
     syms = torch.empty(n, dtype=dt, device="cuda")
-    gt.dev_gen_iid(seed, rank * n, n, syms, sym_bytes, stream)  # this rank's slice of the global array
+    gt.dev_gen_iid(seed, start, n, syms, sym_bytes, stream)  # this rank's slice of the global array
     slots = torch.empty(nchunks * cap, dtype=torch.uint8, device="cuda")
     lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
     status = torch.zeros(1, dtype=torch.int32, device="cuda")
@@ -258,7 +270,7 @@ def main():
         raise SystemExit(f"rank {rank}: round trip failed ({msg})")
     elapsed = float(t[0].item())
     ms_per_step = 1e3 * elapsed / args.steps
-    total_sym_bytes = world * n * sym_bytes
+    total_sym_bytes = total_n * sym_bytes
     value = total_sym_bytes / (elapsed / args.steps) / 2**30
 
     alg_bytes = n * sym_bytes + comp_bytes  # per launch, encode and decode alike
@@ -267,7 +279,8 @@ def main():
         ("_w" if gt.paths() & A.ANS_PATH_ENC_WIDE else "")
     dom_kernel = f"k_{dom_name}{suffix}"
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    rec, rec_src = pmc_record(dom_kernel, args.config, log2n, L)
+    # the PMC records are per-rank workloads of 2^log2n symbols (not a strong-scaling share)
+    rec, rec_src = (None, None) if (args.strong and world > 1) else pmc_record(dom_kernel, args.config, log2n, L)
     traffic = None if rec is None else rec.get("hbm_bytes_per_launch")
     valu = None
     if rec is not None and "valu_per_wave" in rec.get("derived", {}):
@@ -296,12 +309,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (counter-based splitmix64 iid symbols generated on device, SURVEY.md §8d)",
             "config": {
-                "workload": f"{args.config.upper()}: 2^{log2n} iid u{8 * sym_bytes} symbols per GPU, "
+                "workload": f"{args.config.upper()}: 2^{log2n} iid u{8 * sym_bytes} symbols "
+                            f"{'in total' if args.strong else 'per GPU'}, "
                             f"{len(masses)}-symbol Categorical (norm {int(masses.sum())}), chunk_len {L}",
                 "symbols_per_gpu": n,
                 "symbol_bytes": sym_bytes,
@@ -325,6 +339,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),  # vs 6.29 TB/s float4 copy
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_over_alg": None if traffic is None else round(traffic / alg_bytes, 3),
                 "traffic_src": rec_src,

@@ -1064,6 +1064,28 @@ def c3_masses():
     return (np.uint64(1) + (splitmix64_np(np.uint64(0x5EED) ^ s) & np.uint64((1 << 20) - 1))).astype(np.uint64)
 
 
+def c3_pow2_masses():
+    """C3's table quantised to norm 2^24 (SURVEY.md §8d secondary C3): largest-remainder
+    rounding of c3_masses() * 2^24 / norm, every mass at least 1."""
+    m = c3_masses().astype(np.float64)
+    target = 1 << 24
+    exact = m * target / m.sum()
+    q = np.maximum(1, np.floor(exact)).astype(np.int64)
+    rem = target - int(q.sum())
+    order = np.argsort(-(exact - np.floor(exact)))
+    i = 0
+    while rem != 0:
+        k = order[i % len(order)]
+        if rem > 0:
+            q[k] += 1
+            rem -= 1
+        elif q[k] > 1:
+            q[k] -= 1
+            rem += 1
+        i += 1
+    return q.astype(np.uint64)
+
+
 def c4_masses():
     """65,536 masses 1 + (splitmix64(0xC4 ^ s) mod 2^12): norm 134,561,356."""
     s = np.arange(65536, dtype=np.uint64)

@@ -305,6 +305,14 @@ def test_c3_one_gib_u8_round_trip(gpu):
     assert 0.95 < bps < 0.99  # H = 7.738 bits -> ~0.967 B/symbol plus per-chunk flush
 
 
+def test_c3_pow2_norm_bit_exact(gpu):
+    # SURVEY.md §8d secondary C3: the table quantised to norm 2^24 (bench.py --config c3p2)
+    masses = A.c3_pow2_masses()
+    assert int(masses.sum()) == 1 << 24 and int(masses.min()) >= 1
+    syms = orc.gen_iid(masses, 1, 0, 300 * 4096 + 17)
+    _roundtrip_vs_oracle(gpu, masses, syms, 4096, np.uint8)
+
+
 def test_c4_shard_u16_round_trip(gpu):
     # SURVEY.md §8d C4 table (65,536 symbols, norm 134,561,356); one 2^27-symbol shard, all chunks
     total = _device_roundtrip(gpu, A.c4_masses(), 1 << 27, 4096, 2, 2)
