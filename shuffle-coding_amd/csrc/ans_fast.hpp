@@ -52,6 +52,12 @@ constexpr uint32_t kDecNbMax = (kDecTableBytes - 4 * 261 - 16) / 17;
 constexpr uint32_t kDecS0Off = 16 * kDecNbMax;
 constexpr uint32_t kDecCumOff = (kDecS0Off + kDecNbMax + 15) & ~15u;
 static_assert(kDecCumOff + 4 * 261 <= kDecTableBytes, "decode tables fit");
+// the no-far decoder's LDS layout (staged from the same global image): the two inner
+// boundaries (cdf(s0+1), cdf(s0+2)) of each bucket as one 8-B array, the s0 bytes, then one
+// 8-B row (cdf(s), pmf(s)) per symbol
+constexpr uint32_t kDecS0OffR = 8 * kDecNbMax;
+constexpr uint32_t kDecRowOff = (kDecS0OffR + kDecNbMax + 15) & ~15u;
+static_assert(kDecRowOff + 8 * 257 <= kDecTableBytes, "row decode tables fit");
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // Non-temporal 16-byte global load / store (streamed data that must not evict cached tables).
@@ -582,12 +588,20 @@ __host__ __device__ inline uint32_t renorm_screen(uint64_t L) {
     return h > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(h);
 }
 // q = head / norm, cf = head % norm (src/ans.rs:110-111): estimate, then one fix-up
+// The estimate's raw f64 bits are q' + 0x43300000'00000000; q = q' - [ii < 0] and the exponent
+// come off in ONE 64-bit add of (m - 0x43300000 : m), m = ii >> 31 (0 or -1), where the compiler
+// emitted the sign extension, the 64-bit add and a separate v_add for the exponent word.
 __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rcp_norm, uint64_t& qq, uint32_t& cf) {
-    const uint64_t q = qest(head, rcp_norm);
-    const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(q) * norm);
-    const uint32_t neg = ii < 0 ? 1u : 0u;
-    qq = q - neg;
-    cf = static_cast<uint32_t>(ii) + (neg ? norm : 0u);
+    double hd;
+    asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
+    const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
+    const double t = __builtin_fma(xd, rcp_norm, 4503599627370496.0);
+    const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(t));
+    const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(raw) * norm);
+    const uint32_t m = static_cast<uint32_t>(ii >> 31);
+    cf = static_cast<uint32_t>(ii) + (norm & m);
+    const uint64_t adj = mk64(m + 0xBCD00000u, m);  // -0x43300000'00000000 - [ii < 0]
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(qq) : "v"(raw), "v"(adj));
 }
 
 // Stream bytes below the stream start (sh > 0: another chunk's bytes in a dense container)
@@ -762,32 +776,26 @@ struct DecChain {
         sx = s0 + (b1 ? 1u : 0u) + (b2 ? 1u : 0u);
         far = cf >= c.w;
     }
-    // lookup for tables with no far case (kFar = false): the two selects in VOP2 form, each
-    // compare's mask in VCC (the compiler keeps both masks in SGPR pairs for the unit's end and
-    // emits every select, and the symbol's two 0/1 terms, as 64-bit-encoded VOP3), and the
-    // symbol offset t = b1 + b2 by a v_addc whose carry-in is the second mask; sx = s0 + t is
-    // formed off the chain.  s_nop 1: VALU-written VCC read as a lane mask (gfx950 hazard).
-    __device__ __forceinline__ void lookup_nofar(uint32_t shift, uint32_t one) {
+    // no-far lookup through the symbol's row: s = s0 + [cf >= cdf(s0+1)] + [cf >= cdf(s0+2)]
+    // by two v_addc on the compare masks, then (cdf(s), pmf(s)) in one ds_read_b64 of row s:
+    // a second, dependent LDS read in place of six selects
+    __device__ __forceinline__ void lookup_rows(uint32_t shift) {
         const uint32_t bi = cf >> shift;
-        const uint64_t ca = lds_ld64(bi << 3), cb = lds_ld64((bi << 3) + 8 * kDecNbMax);
-        const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0Off));
-        uint32_t t;
+        const uint64_t cc = lds_ld64(bi << 3);
+        const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0OffR));
         asm volatile(
             "v_cmp_ge_u32 vcc, %[cf], %[c1]\n\t"
             "s_nop 1\n\t"
-            "v_cndmask_b32 %[cum], %[c0], %[c1], vcc\n\t"
-            "v_cndmask_b32 %[nxt], %[c1], %[c2], vcc\n\t"
-            "v_cndmask_b32 %[t], 0, %[one], vcc\n\t"
+            "v_addc_co_u32 %[sx], vcc, 0, %[s0], vcc\n\t"
             "v_cmp_ge_u32 vcc, %[cf], %[c2]\n\t"
             "s_nop 1\n\t"
-            "v_cndmask_b32 %[cum], %[cum], %[c2], vcc\n\t"
-            "v_cndmask_b32 %[nxt], %[nxt], %[c3], vcc\n\t"
-            "v_addc_co_u32 %[t], vcc, 0, %[t], vcc"
-            : [cum] "=&v"(cum), [nxt] "=&v"(nxt), [t] "=&v"(t)
-            : [cf] "v"(cf), [c0] "v"(lo32(ca)), [c1] "v"(hi32(ca)), [c2] "v"(lo32(cb)), [c3] "v"(hi32(cb)),
-              [one] "v"(one)
+            "v_addc_co_u32 %[sx], vcc, 0, %[sx], vcc"
+            : [sx] "=&v"(sx)
+            : [cf] "v"(cf), [c1] "v"(lo32(cc)), [c2] "v"(hi32(cc)), [s0] "v"(s0)
             : "vcc");
-        sx = s0 + t;
+        const uint64_t row = lds_ld64(kDecRowOff + (sx << 3));
+        cum = lo32(row);
+        nxt = hi32(row);  // pmf(s)
         far = false;
     }
     __device__ __forceinline__ void lookup_far(const uint32_t* lcum) {  // 3+ boundaries in the bucket
@@ -801,9 +809,9 @@ struct DecChain {
     // phase 3: head = p*q + r (src/ans.rs:113-114).  With every mass below 2^24 (kP24) the
     // high word's product hi32(q) * p (hi32(q) < 2^16 in the fast range) is one full-rate
     // v_mad_u32_u24 instead of a second v_mad_u64_u32.
-    template <bool kP24>
+    template <bool kP24, bool kRowP = false>
     __device__ __forceinline__ void update() {
-        const uint32_t p = nxt - cum, a = cf - cum;
+        const uint32_t p = kRowP ? nxt : nxt - cum, a = cf - cum;
         if constexpr (kP24) {
             const uint64_t lo = static_cast<uint64_t>(lo32(qq)) * p + a;
             uint32_t hi;
@@ -828,7 +836,19 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                                                       const uint32_t* __restrict__ vlen = nullptr) {
     extern __shared__ __align__(16) unsigned char lds[];
     unsigned char* tab = lds;  // tables at offset 0, ring after them
-    {
+    constexpr bool kRows = !kFar;  // the no-far lookup reads (cdf(s), pmf(s)) rows
+    if constexpr (kRows) {
+        const uint2* ga = reinterpret_cast<const uint2*>(t.dbkt);  // (cdf(s0), cdf(s0+1)) per bucket
+        const uint2* gb = ga + kDecNbMax;                           // (cdf(s0+2), cdf(s0+3))
+        const uint8_t* gs = reinterpret_cast<const uint8_t*>(t.dbkt) + kDecS0Off;
+        uint2* pr = reinterpret_cast<uint2*>(tab);
+        for (uint32_t i = threadIdx.x; i < kDecNbMax; i += kDecBlock) {
+            pr[i] = make_uint2(ga[i].y, gb[i].x);
+            tab[kDecS0OffR + i] = gs[i];
+        }
+        uint2* rows = reinterpret_cast<uint2*>(tab + kDecRowOff);
+        for (uint32_t i = threadIdx.x; i < t.nsym; i += kDecBlock) rows[i] = make_uint2(t.cum[i], t.cum[i + 1] - t.cum[i]);
+    } else {
         uint4* b = reinterpret_cast<uint4*>(tab);  // buckets and s0 array: dec_cum_off bytes
         const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt);
         for (uint32_t i = threadIdx.x; i < t.dec_cum_off / 16; i += kDecBlock) b[i] = gb[i];
@@ -849,8 +869,6 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
     const uint32_t shift = t.dec_shift;
-    uint32_t one = 1;
-    asm volatile("" : "+v"(one));  // a VGPR holding 1 (lookup_nofar's VOP2 select source)
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
     // a stream longer than its slot is foreign or corrupt: its pages would lie past the slot
@@ -887,9 +905,9 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                 ch.lookup(shift);
                 if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
             } else {
-                ch.lookup_nofar(shift, one);
+                ch.lookup_rows(shift);
             }
-            ch.template update<kP24>();
+            ch.template update<kP24, kRows>();
             put_sym<Sym>(outv, j, ch.sx);
         }
         switch (u & 7) {
