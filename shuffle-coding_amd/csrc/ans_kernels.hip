@@ -828,8 +828,12 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
                 // the shard's 2 waves per SIMD wait on an L2 round trip every step whatever the
                 // prefix covers, and the prefix path's VALU sat on that chain); the ring alone
                 // leaves room for two workgroups per CU when a shard has the chunks for them
-                if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0)
-                    fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0) {
+                    if (ft.pmax < (1u << 24))
+                        fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                    else
+                        fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                }
                 else if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
                     fast::k_decode_w<Sym, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                 else

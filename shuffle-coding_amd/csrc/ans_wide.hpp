@@ -174,6 +174,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         }
     };
 
+#endif
+
     uint4 n[GU];
 #pragma unroll
     for (int i = 0; i < GU; ++i) n[i] = make_uint4(0, 0, 0, 0);
@@ -354,7 +356,19 @@ struct DecChainW {
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
     }
-    __device__ __forceinline__ void update(uint32_t p, uint32_t r) { head = qq * p + r; }
+    // head = p*q + r; with every mass below 2^24 (kP24) the high word's product is one
+    // v_mad_u32_u24 (hi32(q) < 2^16 for norm >= 2^16), as in ans_fast.hpp DecChain::update
+    template <bool kP24>
+    __device__ __forceinline__ void update(uint32_t p, uint32_t r) {
+        if constexpr (kP24) {
+            const uint64_t lo = static_cast<uint64_t>(lo32(qq)) * p + r;
+            uint32_t hi;
+            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(hi) : "v"(hi32(qq)), "v"(p), "v"(hi32(lo)));
+            head = mk64(hi, lo32(lo));
+        } else {
+            head = qq * p + r;
+        }
+    }
 };
 
 // kCompact: the global buckets are DecBucketC (16 B, one L2 request), else DecBucketG (32 B).
@@ -363,7 +377,8 @@ struct DecChainW {
 // which for C4 is nearly every step, so the prefix only added VALU to the chain).
 // kVar: chunk c decodes vlen[c] <= chunk_len symbols into the start of its chunk_len-symbol
 // stride (staged output: the rest of its last 128-B line is garbage).
-template <typename Sym, bool kCompact, bool kPrefix, bool kVar = false>
+// kP24: every mass is below 2^24 (DecChainW::update).
+template <typename Sym, bool kCompact, bool kPrefix, bool kVar = false, bool kP24 = false>
 __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
                                                          uint64_t slot_cap, const uint64_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ lens,
@@ -482,7 +497,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
                 r = cf - cum;
             }
         }
-        ch.update(p, r);  // head = p*q + r (src/ans.rs:113-114)
+        ch.template update<kP24>(p, r);  // head = p*q + r (src/ans.rs:113-114)
         return sx;
     };
 
