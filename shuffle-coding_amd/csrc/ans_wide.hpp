@@ -174,8 +174,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         }
     };
 
-#endif
-
     uint4 n[GU];
 #pragma unroll
     for (int i = 0; i < GU; ++i) n[i] = make_uint4(0, 0, 0, 0);
