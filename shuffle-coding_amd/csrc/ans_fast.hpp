@@ -80,6 +80,17 @@ __device__ __forceinline__ void wait_vm_n() {
     __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
 }
 
+// x << S in 16 bits (the upper half of the result is zero on gfx950): v_lshlrev_b16 issues in
+// ~2.5 cycles per wave64 instruction where v_lshlrev_b32 and its SDWA forms take ~4.4
+// (tools/b16_probe.hip), so LDS addresses below 2^16 are formed with it
+template <int S>
+__device__ __forceinline__ uint32_t shl16(uint32_t x) {
+    static_assert(S >= 0 && S < 16, "16-bit shift");
+    uint32_t r;
+    asm("v_lshlrev_b16 %0, %1, %2" : "=v"(r) : "I"(S), "v"(x));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
 }
@@ -221,7 +232,7 @@ struct FunnelT {
         *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + kBase)) = d0;
         pos8 += k8;
         neg8 -= k8;
-        const uint32_t a = ((pos8 << 6) & 0xF800u) | col;
+        const uint32_t a = (shl16<6>(pos8) & 0xF800u) | col;  // (pos8 << 6) & 0xF800 needs 16 bits
         X = a != addr ? d1 : d0;
         addr = a;
     }
@@ -785,7 +796,7 @@ struct DecChain {
     // a second, dependent LDS read in place of six selects
     __device__ __forceinline__ void lookup_rows(uint32_t shift) {
         const uint32_t bi = cf >> shift;
-        const uint64_t cc = lds_ld64(bi << 3);
+        const uint64_t cc = lds_ld64(shl16<3>(bi));  // bi < kDecNbMax
         const uint32_t s0 = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(bi + kDecS0OffR));
         asm volatile(
             "v_cmp_ge_u32 vcc, %[cf], %[c1]\n\t"
@@ -797,7 +808,7 @@ struct DecChain {
             : [sx] "=&v"(sx)
             : [cf] "v"(cf), [c1] "v"(lo32(cc)), [c2] "v"(hi32(cc)), [s0] "v"(s0)
             : "vcc");
-        const uint64_t row = lds_ld64(kDecRowOff + (sx << 3));
+        const uint64_t row = lds_ld64(kDecRowOff + shl16<3>(sx));  // sx < 256
         cum = lo32(row);
         nxt = hi32(row);  // pmf(s)
         far = false;
