@@ -900,40 +900,58 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     // symbols leave in whole 128-B lines per lane (eight units): a 64-B store leaves its line
     // half-written in L2 for a block, where the streaming reads can evict it in pieces
     uint4 q[8];
-    for (int u = 0; u < nunit; ++u) {
-        uint4 outv = make_uint4(0, 0, 0, 0);
+    // eight units per iteration, unrolled, so each unit's symbols go straight into their q[]
+    // registers (a unit index known only at run time made the compiler copy the line through
+    // a branch tree of v_mov, ~20 per unit)
+    for (int u0 = 0; u0 < nunit; u0 += 8) {
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-            if (j % SPP == 0) {
-                wait_vm();  // point: retire what the previous point issued
-                if (j == 0 && u > 0 && (u & 7) == 0) {
-                    uint4* d = dst + (u - 8);
+        for (int uu = 0; uu < 8; ++uu) {
+            const int u = u0 + uu;
+            if (u < nunit) {  // (uniform unless staged)
+                uint32_t sv[U];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) d[k] = q[k];
+                for (int j = 0; j < U; ++j) {
+                    sv[j] = 0;
+                    if (j % SPP == 0) {
+                        wait_vm();  // point: retire what the previous point issued
+                        if (j == 0 && uu == 0 && u0 > 0) {
+                            uint4* d = dst + (u0 - 8);
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) d[k] = q[k];
+                        }
+                        ch.point();
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
+                    ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
+                    if constexpr (kFar) {
+                        ch.lookup(shift);
+                        if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+                    } else {
+                        ch.lookup_rows(shift);
+                    }
+                    ch.template update<kP24, kRows>();
+                    sv[j] = ch.sx;
                 }
-                ch.point();
+                uint4 outv = make_uint4(0, 0, 0, 0);
+                if constexpr (sizeof(Sym) == 1) {  // three v_lshl_or per dword
+                    uint32_t w[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        uint32_t x;
+                        asm("v_lshl_or_b32 %0, %1, 8, %2\n\t"
+                            "v_lshl_or_b32 %0, %3, 16, %0\n\t"
+                            "v_lshl_or_b32 %0, %4, 24, %0"
+                            : "=&v"(x) : "v"(sv[4 * k + 1]), "v"(sv[4 * k]), "v"(sv[4 * k + 2]), "v"(sv[4 * k + 3]));
+                        w[k] = x;
+                    }
+                    outv = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < U; ++j) put_sym<Sym>(outv, j, sv[j]);
+                }
+                q[uu] = outv;
             }
-            __builtin_amdgcn_sched_barrier(0);  // one step at a time: cross-step interleaving only spills SGPRs
-            if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
-            ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
-            if constexpr (kFar) {
-                ch.lookup(shift);
-                if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
-            } else {
-                ch.lookup_rows(shift);
-            }
-            ch.template update<kP24, kRows>();
-            put_sym<Sym>(outv, j, ch.sx);
-        }
-        switch (u & 7) {
-        case 0: q[0] = outv; break;
-        case 1: q[1] = outv; break;
-        case 2: q[2] = outv; break;
-        case 3: q[3] = outv; break;
-        case 4: q[4] = outv; break;
-        case 5: q[5] = outv; break;
-        case 6: q[6] = outv; break;
-        default: q[7] = outv; break;
         }
     }
     wait_vm();
