@@ -703,8 +703,15 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
 #define DECV(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4, true><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
 #define DECV_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DECV(SPP, FAR, true, J4); else DECV(SPP, FAR, false, J4)
 #define DECV_J(SPP, FAR) if (ft.kmax >= 4) { DECV_P(SPP, FAR, true); } else { DECV_P(SPP, FAR, false); }
-            if (U * ft.kmax > 60) {
-                if (ft.dec_far) { DECV_P(U / 2, true, true); } else { DECV_P(U / 2, false, true); }
+            // only the combinations a table can select are instantiated: u8 (U = 16) takes
+            // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
+            constexpr bool kHalf = U * 4 > 60;
+            if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
+                if constexpr (kHalf) {
+                    if (ft.dec_far) { DECV_P(U / 2, true, true); } else { DECV_P(U / 2, false, true); }
+                }
+            } else if constexpr (kHalf) {  // kmax <= 3
+                if (ft.dec_far) { DECV_P(U, true, false); } else { DECV_P(U, false, false); }
             } else {
                 if (ft.dec_far) { DECV_J(U, true); } else { DECV_J(U, false); }
             }
@@ -845,8 +852,15 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
 #define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
 #define DEC_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true, J4); else DEC(SPP, FAR, false, J4)
 #define DEC_J(SPP, FAR) if (ft.kmax >= 4) { DEC_P(SPP, FAR, true); } else { DEC_P(SPP, FAR, false); }
-            if (U * ft.kmax > 60) {  // (kmax = 4)
-                if (ft.dec_far) { DEC_P(U / 2, true, true); } else { DEC_P(U / 2, false, true); }
+            // only the combinations a table can select are instantiated: u8 (U = 16) takes
+            // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
+            constexpr bool kHalf = U * 4 > 60;
+            if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
+                if constexpr (kHalf) {
+                    if (ft.dec_far) { DEC_P(U / 2, true, true); } else { DEC_P(U / 2, false, true); }
+                }
+            } else if constexpr (kHalf) {  // kmax <= 3
+                if (ft.dec_far) { DEC_P(U, true, false); } else { DEC_P(U, false, false); }
             } else {
                 if (ft.dec_far) { DEC_J(U, true); } else { DEC_J(U, false); }
             }
