@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 
 #include "ans_table.hpp"
 
@@ -89,6 +90,13 @@ __device__ __forceinline__ uint32_t shl16(uint32_t x) {
     uint32_t r;
     asm("v_lshlrev_b16 %0, %1, %2" : "=v"(r) : "I"(S), "v"(x));
     return r;
+}
+
+// f(integral_constant<int, I>) for each I in order, every call inlined: a loop unrolled by
+// construction, so register arrays indexed by I stay in registers
+template <typename F, int... I>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
 }
 
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t s) {
@@ -904,8 +912,10 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     // registers (a unit index known only at run time made the compiler copy the line through
     // a branch tree of v_mov, ~20 per unit)
     for (int u0 = 0; u0 < nunit; u0 += 8) {
-#pragma unroll
-        for (int uu = 0; uu < 8; ++uu) {
+        // the eight units as eight inlined calls with a compile-time index (a #pragma unroll
+        // over them is refused for the larger instantiations, which then index q[] in scratch)
+        auto unit = [&](auto ic) __attribute__((always_inline)) {
+            constexpr int uu = decltype(ic)::value;
             const int u = u0 + uu;
             if (u < nunit) {  // (uniform unless staged)
                 uint32_t sv[U];
@@ -952,7 +962,8 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                 }
                 q[uu] = outv;
             }
-        }
+        };
+        unroll_seq(unit, std::make_integer_sequence<int, 8>{});
     }
     wait_vm();
     if (nunit > 0) {  // the last (partial) line: 4 or 8 units (chunk bytes % 64 == 0; staged: all 8)
