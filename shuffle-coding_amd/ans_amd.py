@@ -740,12 +740,17 @@ class GpuTable:
                "ans_dev_encode_chunks")
 
     def dev_encode_dense(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_offsets, d_out,
-                         d_status, stream=None, gen_kind=GEN_ZEROS, seed=0):
+                         d_status, stream=None, gen_kind=GEN_ZEROS, seed=0, out_cap=None):
         """Device-resident dense container (ans_dev_encode_dense_ex): d_offsets holds
-        dense_offsets_entries(nchunks) u64 entries; chunk j at d_out[d_offsets[j]:][:d_lens[j]]."""
+        dense_offsets_entries(nchunks) u64 entries; chunk j at d_out[d_offsets[j]:][:d_lens[j]].
+        out_cap: d_out's size in bytes (default: the tensor's; required for a raw pointer)."""
+        if out_cap is None:
+            if isinstance(d_out, int):
+                raise ValueError("dev_encode_dense: out_cap is required when d_out is a raw device pointer")
+            out_cap = _nbytes(d_out)
         _check(lib().ans_dev_encode_dense_ex(self.h, _dptr(d_syms), sym_bytes, n, chunk_len, gen_kind, seed,
                                              _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_offsets), _dptr(d_out),
-                                             _nbytes(d_out), _dptr(d_status), _sptr(stream)), "ans_dev_encode_dense")
+                                             int(out_cap), _dptr(d_status), _sptr(stream)), "ans_dev_encode_dense")
 
     def dev_decode(self, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status,
                    stream=None, gen_kind=GEN_ZEROS, seed=0):

@@ -60,6 +60,20 @@ static_assert(kDecCumOff + 4 * 261 <= kDecTableBytes, "decode tables fit");
 constexpr uint32_t kDecS0OffR = 8 * kDecNbMax;
 constexpr uint32_t kDecRowOff = (kDecS0OffR + kDecNbMax + 15) & ~15u;
 static_assert(kDecRowOff + 8 * 257 <= kDecTableBytes, "row decode tables fit");
+// the fix-up-free decoder's LDS layout (k_decode kMode = kModeU, FastTable::dec_u): the quotient
+// from below (q_m in {q - 1, q}) leaves u = head - q_m * norm in [0, 2 norm), which indexes a
+// virtual alphabet of 512 symbols: v < 256 is symbol v at cdf(v) (q = q_m), v >= 256 symbol
+// v - 256 at norm + cdf(v - 256) (q = q_m + 1).  Buckets of u as (cdfv(s0+1), cdfv(s0+2))
+// pairs, their u16 s0 values, then 512 rows (cum_row, p) with head = p * q_m + (u - cum_row).
+constexpr uint32_t kDecUNbMax = (kDecTableBytes - 8 * 512) / 10;
+constexpr uint32_t kDecUS0Off = 8 * kDecUNbMax;
+constexpr uint32_t kDecURowOff = (kDecUS0Off + 2 * kDecUNbMax + 15) & ~15u;
+static_assert(kDecURowOff + 8 * 512 <= kDecTableBytes, "u-domain decode tables fit");
+static_assert(kDecUS0Off + 2 * kDecUNbMax <= 65535 && kDecURowOff <= 65535, "ds offsets");
+// decode lookup modes (k_decode kMode)
+constexpr int kModeFar = 0;   // 16-B buckets, three candidates, voted scan of the staged cdf
+constexpr int kModeRows = 1;  // 8-B buckets, two boundaries, then the symbol's (cdf, pmf) row
+constexpr int kModeU = 2;     // kModeRows over u in [0, 2 norm): no quotient fix-up
 constexpr uint64_t kMaxMinHead = 1ull << 56;
 
 // Non-temporal 16-byte global load / store (streamed data that must not evict cached tables).
@@ -780,6 +794,39 @@ struct DecChain {
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
     }
+    // phase 1 for kModeU: the quotient from below, q_m = qq's low word and hi = hi32(q_m) (no
+    // fix-up: u = head - q_m * norm in [0, 2 norm) goes to the u-domain tables as it is)
+    template <bool kJ4>
+    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
+        form_window();
+        P -= static_cast<int32_t>(renorm_up<kJ4>(head, W, L, hL8));
+        read_window();  // for the next step; kept ahead of this step's bucket reads
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t raw = qest_m1(head, rcp_norm);  // q_m + 0x43300000'00000000
+        cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
+        qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
+    }
+    // the u-domain icdf: bucket u >> shift -> (cdfv(s0+1), cdfv(s0+2)) and s0 (u16), the virtual
+    // symbol v = s0 + [u >= cdfv(s0+1)] + [u >= cdfv(s0+2)], then its row (cum_row, p)
+    __device__ __forceinline__ void lookup_u(uint32_t shift) {
+        const uint32_t bi = cf >> shift;
+        const uint64_t cc = lds_ld64(shl16<3>(bi));  // bi < kDecUNbMax
+        const uint32_t s0 = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(shl16<1>(bi) + kDecUS0Off));
+        asm volatile(
+            "v_cmp_ge_u32 vcc, %[cf], %[c1]\n\t"
+            "s_nop 1\n\t"
+            "v_addc_co_u32 %[sx], vcc, 0, %[s0], vcc\n\t"
+            "v_cmp_ge_u32 vcc, %[cf], %[c2]\n\t"
+            "s_nop 1\n\t"
+            "v_addc_co_u32 %[sx], vcc, 0, %[sx], vcc"
+            : [sx] "=&v"(sx)
+            : [cf] "v"(cf), [c1] "v"(lo32(cc)), [c2] "v"(hi32(cc)), [s0] "v"(s0)
+            : "vcc");
+        const uint64_t row = lds_ld64(kDecURowOff + shl16<3>(sx));  // sx < 512
+        cum = lo32(row);
+        nxt = hi32(row);  // pmf(s)
+        far = false;
+    }
     // phase 2: icdf (src/codec.rs:65-68), the last symbol with cdf <= cf, from cf's bucket:
     // c0..c3 in one ds_read_b128 (two compares pick among three candidates; cf >= c3 is the
     // voted far case), s0 from the array after the buckets.
@@ -847,10 +894,12 @@ struct DecChain {
 };
 
 // SPP: symbols per point (U, or U/2 when U*KMAX > 60: u8 tables whose pops can take 4 bytes).
-// kFar: some bucket holds more than four cdf boundaries, so the voted slow path is compiled in.
+// kMode: the icdf (kModeFar: some bucket holds more than four cdf boundaries, so the voted slow
+// path is compiled in; kModeRows: every bucket resolves among three candidates, then the
+// symbol's row; kModeU: kModeRows over u = head - q_m * norm, no quotient fix-up).
 // kP24: every mass is below 2^24 (DecChain::update).  kJ4: some pop can pull 4 bytes (kmax = 4).
 // kVar: chunk c decodes vlen[c] <= chunk_len symbols into the start of its stride (staged output).
-template <typename Sym, int SPP, bool kFar, bool kP24, bool kJ4, bool kVar = false>
+template <typename Sym, int SPP, int kMode, bool kP24, bool kJ4, bool kVar = false>
 __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint64_t* __restrict__ offsets,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
@@ -859,8 +908,13 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                                                       const uint32_t* __restrict__ vlen = nullptr) {
     extern __shared__ __align__(16) unsigned char lds[];
     unsigned char* tab = lds;  // tables at offset 0, ring after them
-    constexpr bool kRows = !kFar;  // the no-far lookup reads (cdf(s), pmf(s)) rows
-    if constexpr (kRows) {
+    constexpr bool kFar = kMode == kModeFar;
+    constexpr bool kRows = !kFar;  // the no-far lookups read (cum, pmf) rows
+    if constexpr (kMode == kModeU) {  // the u-domain image is the LDS layout itself
+        const uint4* g = reinterpret_cast<const uint4*>(t.dec_u_img);
+        uint4* d = reinterpret_cast<uint4*>(tab);
+        for (uint32_t i = threadIdx.x; i < kDecTableBytes / 16; i += kDecBlock) d[i] = g[i];
+    } else if constexpr (kRows) {
         const uint2* ga = reinterpret_cast<const uint2*>(t.dbkt);  // (cdf(s0), cdf(s0+1)) per bucket
         const uint2* gb = ga + kDecNbMax;                           // (cdf(s0+2), cdf(s0+3))
         const uint8_t* gs = reinterpret_cast<const uint8_t*>(t.dbkt) + kDecS0Off;
@@ -891,7 +945,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
-    const uint32_t shift = t.dec_shift;
+    const uint32_t shift = kMode == kModeU ? t.dec_u_shift : t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
     // a stream longer than its slot is foreign or corrupt: its pages would lie past the slot
@@ -933,18 +987,35 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
-                    ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
-                    if constexpr (kFar) {
-                        ch.lookup(shift);
-                        if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+                    if constexpr (kMode == kModeU) {
+                        ch.template renorm_div_u<kJ4>(L, hL8, norm, rcp_norm);
+                        ch.lookup_u(shift);
                     } else {
-                        ch.lookup_rows(shift);
+                        ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
+                        if constexpr (kFar) {
+                            ch.lookup(shift);
+                            if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);
+                        } else {
+                            ch.lookup_rows(shift);
+                        }
                     }
                     ch.template update<kP24, kRows>();
-                    sv[j] = ch.sx;
+                    sv[j] = ch.sx;  // kModeU: the virtual symbol (its low byte is the symbol)
                 }
                 uint4 outv = make_uint4(0, 0, 0, 0);
-                if constexpr (sizeof(Sym) == 1) {  // three v_lshl_or per dword
+                if constexpr (sizeof(Sym) == 1 && kMode == kModeU) {  // the low bytes, by v_perm: two per dword and an or
+                    uint32_t w[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t lo = __builtin_amdgcn_perm(sv[4 * k + 1], sv[4 * k], 0x0C0C0400u);
+                        const uint32_t hi = __builtin_amdgcn_perm(sv[4 * k + 3], sv[4 * k + 2], 0x04000C0Cu);
+                        w[k] = lo | hi;
+                    }
+                    outv = make_uint4(w[0], w[1], w[2], w[3]);
+                } else if constexpr (kMode == kModeU) {
+#pragma unroll
+                    for (int j = 0; j < U; ++j) put_sym<Sym>(outv, j, sv[j] & 0xFFu);
+                } else if constexpr (sizeof(Sym) == 1) {  // three v_lshl_or per dword
                     uint32_t w[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {

@@ -637,7 +637,10 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
         const uint64_t lpad = std::max<uint64_t>(GS, (lmax + GS - 1) / GS * GS);
         void* mem = nullptr;
         const size_t stage_b = nchunks * lpad * sizeof(Sym), vlen_o = (stage_b + 255) & ~size_t(255);
-        HIP_TRY(hipMallocAsync(&mem, vlen_o + 4 * nchunks, s));
+        if (hipMallocAsync(&mem, vlen_o + 4 * nchunks, s) != hipSuccess) {
+            (void)hipGetLastError();  // no room to stage: the generic kernels need none
+            return kNotStaged;
+        }
         Sym* stage = static_cast<Sym*>(mem);
         uint32_t* vlen = reinterpret_cast<uint32_t*>(static_cast<char*>(mem) + vlen_o);
         const uint64_t units = nchunks * lpad / (16 / sizeof(Sym));
@@ -685,7 +688,10 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
         const uint64_t lpad = std::max<uint64_t>(GS, (lmax + GS - 1) / GS * GS);
         void* mem = nullptr;
         const size_t stage_b = nchunks * lpad * sizeof(Sym), vlen_o = (stage_b + 255) & ~size_t(255);
-        HIP_TRY(hipMallocAsync(&mem, vlen_o + 4 * nchunks, s));
+        if (hipMallocAsync(&mem, vlen_o + 4 * nchunks, s) != hipSuccess) {
+            (void)hipGetLastError();  // no room to stage: the generic kernels need none
+            return kNotStaged;
+        }
         Sym* stage = static_cast<Sym*>(mem);
         uint32_t* vlen = reinterpret_cast<uint32_t*>(static_cast<char*>(mem) + vlen_o);
         const uint64_t units = nchunks * lpad / (16 / sizeof(Sym));
@@ -700,22 +706,22 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nchunks + fast::kDecBlock - 1) / fast::kDecBlock);
             constexpr int U = 16 / sizeof(Sym);
-#define DECV(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4, true><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
-#define DECV_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DECV(SPP, FAR, true, J4); else DECV(SPP, FAR, false, J4)
-#define DECV_J(SPP, FAR) if (ft.kmax >= 4) { DECV_P(SPP, FAR, true); } else { DECV_P(SPP, FAR, false); }
+#define DECV(SPP, MODE, P24, J4) fast::k_decode<Sym, SPP, MODE, P24, J4, true><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
+#define DECV_P(SPP, MODE, J4) if (ft.pmax < (1u << 24)) DECV(SPP, MODE, true, J4); else DECV(SPP, MODE, false, J4)
+#define DECV_M(SPP, J4) if (ft.dec_far) { DECV_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DECV_P(SPP, fast::kModeU, J4); } else { DECV_P(SPP, fast::kModeRows, J4); }
             // only the combinations a table can select are instantiated: u8 (U = 16) takes
             // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
             constexpr bool kHalf = U * 4 > 60;
             if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
-                if constexpr (kHalf) {
-                    if (ft.dec_far) { DECV_P(U / 2, true, true); } else { DECV_P(U / 2, false, true); }
-                }
+                if constexpr (kHalf) { DECV_M(U / 2, true); }
             } else if constexpr (kHalf) {  // kmax <= 3
-                if (ft.dec_far) { DECV_P(U, true, false); } else { DECV_P(U, false, false); }
+                DECV_M(U, false);
+            } else if (ft.kmax >= 4) {
+                DECV_M(U, true);
             } else {
-                if (ft.dec_far) { DECV_J(U, true); } else { DECV_J(U, false); }
+                DECV_M(U, false);
             }
-#undef DECV_J
+#undef DECV_M
 #undef DECV_P
 #undef DECV
         }
@@ -743,7 +749,10 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
     if (nchunks == 0) return ANS_OK;
     const DevTable& t = gt->t;
     const Sym* syms = static_cast<const Sym*>(d_syms);
-    if ((chunk_len * sizeof(Sym)) % 128 != 0 && staged_encode_ok<Sym>(gt)) {  // ragged chunks (C2)
+    // ragged chunks (C2): staged when the padded layout stays within staged_lmax's budget (short
+    // chunks pad to 128 B each: chunk_len 1 would stage 128x the symbols)
+    if ((chunk_len * sizeof(Sym)) % 128 != 0 && staged_encode_ok<Sym>(gt) &&
+        staged_lmax(nchunks, chunk_len, n, sizeof(Sym)) != 0) {
         const int rc = launch_staged_encode<Sym>(gt, syms, ChunkSpan<Sym>{nullptr, chunk_len, n}, nchunks, chunk_len,
                                                  d_slots, slot_cap, d_lens, d_status, s, ini);
         if (rc != kNotStaged) return rc;
@@ -814,7 +823,8 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const DevTable& t = gt->t;
     const FastTable& ft = gt->ft;
     Sym* out = static_cast<Sym*>(d_syms);
-    if ((chunk_len * sizeof(Sym)) % 64 != 0 && staged_decode_ok<Sym>(gt)) {  // ragged chunks (C2)
+    if ((chunk_len * sizeof(Sym)) % 64 != 0 && staged_decode_ok<Sym>(gt) &&
+        staged_lmax(nchunks, chunk_len, n, sizeof(Sym)) != 0) {  // ragged chunks (C2), within the budget
         const int rc = launch_staged_decode<Sym>(gt, d_in, d_offsets, slot_cap, d_lens, ChunkSpan<Sym>{nullptr, chunk_len, n},
                                                  nchunks, chunk_len, gen_kind, out, d_status, s, ini);
         if (rc != kNotStaged) return rc;
@@ -849,22 +859,22 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
-#define DEC(SPP, FAR, P24, J4) fast::k_decode<Sym, SPP, FAR, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
-#define DEC_P(SPP, FAR, J4) if (ft.pmax < (1u << 24)) DEC(SPP, FAR, true, J4); else DEC(SPP, FAR, false, J4)
-#define DEC_J(SPP, FAR) if (ft.kmax >= 4) { DEC_P(SPP, FAR, true); } else { DEC_P(SPP, FAR, false); }
+#define DEC(SPP, MODE, P24, J4) fast::k_decode<Sym, SPP, MODE, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
+#define DEC_P(SPP, MODE, J4) if (ft.pmax < (1u << 24)) DEC(SPP, MODE, true, J4); else DEC(SPP, MODE, false, J4)
+#define DEC_M(SPP, J4) if (ft.dec_far) { DEC_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DEC_P(SPP, fast::kModeU, J4); } else { DEC_P(SPP, fast::kModeRows, J4); }
             // only the combinations a table can select are instantiated: u8 (U = 16) takes
             // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
             constexpr bool kHalf = U * 4 > 60;
             if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
-                if constexpr (kHalf) {
-                    if (ft.dec_far) { DEC_P(U / 2, true, true); } else { DEC_P(U / 2, false, true); }
-                }
+                if constexpr (kHalf) { DEC_M(U / 2, true); }
             } else if constexpr (kHalf) {  // kmax <= 3
-                if (ft.dec_far) { DEC_P(U, true, false); } else { DEC_P(U, false, false); }
+                DEC_M(U, false);
+            } else if (ft.kmax >= 4) {
+                DEC_M(U, true);
             } else {
-                if (ft.dec_far) { DEC_J(U, true); } else { DEC_J(U, false); }
+                DEC_M(U, false);
             }
-#undef DEC_J
+#undef DEC_M
 #undef DEC_P
 #undef DEC
         }
@@ -1053,6 +1063,58 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             d.pad = 0;
         }
     }
+    // the fix-up-free decoder's tables (ans_fast.hpp kModeU): the virtual alphabet over
+    // u in [0, 2 norm) (v < 256: symbol v at cdf(v); v >= 256: symbol v - 256 at norm + cdf),
+    // at the finest bucket width that fits; kept only if every bucket resolves among three
+    // candidates (a table with fewer than 256 symbols can leave a bucket straddling u = norm
+    // with the zero-mass gap between the halves: those keep the kModeRows tables)
+    std::vector<uint8_t> uimg;
+    if (ft.dec_usable && !ft.dec_far && t.norm < (1u << 31)) {
+        const uint64_t n2 = 2ull * t.norm;
+        auto cdfv = [&](uint32_t v) -> uint64_t {
+            if (v >= 512) return n2;
+            const uint32_t sv = v & 255u;
+            const uint64_t c = cum[std::min(sv, nsym)];
+            return v < 256 ? c : t.norm + c;
+        };
+        auto icdfv = [&](uint64_t x) {  // the last v in [0, 512) with cdfv(v) <= x
+            uint32_t lo = 0, hi = 511;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (cdfv(mid) <= x) lo = mid;
+                else hi = mid - 1;
+            }
+            return lo;
+        };
+        uint32_t us = 0;
+        while (((n2 - 1) >> us) + 1 > fast::kDecUNbMax) ++us;
+        const uint32_t nbu = static_cast<uint32_t>(((n2 - 1) >> us) + 1);
+        uimg.assign(fast::kDecTableBytes, 0);
+        bool ok = true;
+        for (uint32_t j = 0; j < nbu && ok; ++j) {
+            const uint64_t a = static_cast<uint64_t>(j) << us, end = std::min<uint64_t>(n2, a + (1ull << us));
+            const uint32_t s0 = icdfv(a);
+            if (cdfv(s0 + 3) < end) ok = false;
+            const uint32_t c12[2] = {static_cast<uint32_t>(cdfv(s0 + 1)), static_cast<uint32_t>(cdfv(s0 + 2))};
+            const uint16_t s16 = static_cast<uint16_t>(s0);
+            std::memcpy(uimg.data() + 8 * j, c12, 8);
+            std::memcpy(uimg.data() + fast::kDecUS0Off + 2 * j, &s16, 2);
+        }
+        for (uint32_t v = 0; v < 512 && ok; ++v) {
+            const uint32_t sv = v & 255u;
+            const uint32_t m = sv < nsym ? static_cast<uint32_t>(cat.masses[sv]) : 0u;
+            const uint32_t c = cum[std::min(sv, nsym)];
+            // head = p * q_m + (u - cum_row): lower half q = q_m, cf = u; upper q = q_m + 1, cf = u - norm
+            const uint32_t row[2] = {v < 256 ? c : t.norm + c - m, m};
+            std::memcpy(uimg.data() + fast::kDecURowOff + 8 * v, row, 8);
+        }
+        if (ok) {
+            ft.dec_u = 1;
+            ft.dec_u_shift = us;
+        } else {
+            uimg.clear();
+        }
+    }
     ft.dec_global = !ft.dec_usable;
     // compact 16-B buckets for k_decode_w: the finest width with at most 2^17 buckets (2 MiB),
     // if every bucket's five candidate offsets fit u16
@@ -1190,9 +1252,10 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const size_t decc_b = sizeof(DecBucketC) * decc.size();
     const size_t o_pack = o_decc + ((decc_b + 255) & ~size_t(255));
     const size_t pack_b = sizeof(uint32_t) * pack_img.size();
+    const size_t o_uimg = o_pack + ((pack_b + 255) & ~size_t(255));
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
-    HIP_TRY(hipMalloc(&mem, o_pack + pack_b + 16));
+    HIP_TRY(hipMalloc(&mem, o_uimg + uimg.size() + 16));
     gt->d_fast = mem;
     char* base = static_cast<char*>(mem);
     HIP_TRY(hipMemcpy(base, enc.data(), enc_b, hipMemcpyHostToDevice));
@@ -1212,6 +1275,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dbkt_c = reinterpret_cast<const DecBucketC*>(base + o_decc);
     if (pack_b) HIP_TRY(hipMemcpy(base + o_pack, pack_img.data(), pack_b, hipMemcpyHostToDevice));
     ft.enc_pack_img = reinterpret_cast<const uint32_t*>(base + o_pack);
+    if (!uimg.empty()) HIP_TRY(hipMemcpy(base + o_uimg, uimg.data(), uimg.size(), hipMemcpyHostToDevice));
+    ft.dec_u_img = reinterpret_cast<const uint32_t*>(base + o_uimg);
     ft.dec_w_s0 = reinterpret_cast<const uint16_t*>(base + o_ws0);
     ft.dbkt_g = reinterpret_cast<const DecBucketG*>(base + o_decg);
     ft.enc = reinterpret_cast<const EncRow*>(base);
@@ -2135,8 +2200,51 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
     return ANS_OK;
 }
 
-// lmax > 0 (the longest chunk, known to the host callers): the staged fast kernels where the
-// table has them (launch_staged_encode); the device API passes 0 and keeps the generic kernels
+// The longest variable chunk and the total of device-resident starts (one workgroup: a strided
+// max per lane, a wave shfl_xor reduction, the 16 wave maxima through LDS) -> out[0], out[1].
+__global__ __launch_bounds__(1024) void k_span_stats(const uint64_t* __restrict__ starts, uint64_t nchunks,
+                                                    uint64_t* __restrict__ out) {
+    __shared__ uint64_t part[16];
+    uint64_t m = 0;
+    for (uint64_t c = threadIdx.x; c < nchunks; c += 1024) {
+        const uint64_t a = starts[c], b = starts[c + 1];
+        m = max(m, b >= a ? b - a : ~0ull);  // decreasing starts: no staging (the kernels report them)
+    }
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, static_cast<uint64_t>(__shfl_xor(m, d)));
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) m = max(m, part[w]);
+        out[0] = m;
+        out[1] = starts[nchunks] - starts[0];
+    }
+}
+
+// staged_lmax for device-resident starts: k_span_stats, one 16-B copy back and a stream
+// synchronisation (the device API's variable chunks then take the staged fast kernels, as the
+// host API's do); 0 (the generic kernels) when the staged layout would exceed the budget
+static int device_lmax(const uint64_t* d_starts, uint64_t nchunks, int sym_bytes, hipStream_t s, uint64_t* lmax) {
+    *lmax = 0;
+    if (nchunks == 0) return ANS_OK;
+    void* mem = nullptr;
+    if (hipMallocAsync(&mem, 16, s) != hipSuccess) {
+        (void)hipGetLastError();
+        return ANS_OK;  // the generic kernels
+    }
+    uint64_t h[2] = {0, 0};
+    k_span_stats<<<1, 1024, 0, s>>>(d_starts, nchunks, static_cast<uint64_t*>(mem));
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(h, mem, 16, hipMemcpyDeviceToHost, s);
+    const hipError_t f = hipFreeAsync(mem, s);
+    if (e == hipSuccess) e = f;
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    HIP_TRY(e);
+    *lmax = (h[0] >> 32) ? 0 : staged_lmax(nchunks, h[0], h[1], sym_bytes);
+    return ANS_OK;
+}
+
+// lmax > 0 (the longest chunk): the staged fast kernels where the table has them
+// (launch_staged_encode); the device API finds it with device_lmax
 int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                           const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap,
                           uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax) {
@@ -2159,8 +2267,17 @@ int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_
 int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                                  const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots,
                                  uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();
+    if (!gt || !valid_width(sym_bytes)) return ANS_E_ARG;
+    if (nchunks && !d_starts) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    uint64_t lmax = 0;
+    if (!gt->ts64) {
+        const int rc = device_lmax(d_starts, nchunks, sym_bytes, pick(gt, stream), &lmax);
+        if (rc) return rc;
+    }
     return dev_encode_var(gt, d_syms, sym_bytes, nchunks, d_starts, gen_kind, seed, d_slots, slot_cap, d_lens, d_status,
-                          stream, 0);
+                          stream, lmax);
 }
 
 int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
@@ -2193,8 +2310,17 @@ int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_off
 int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                                  const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
                                  uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+    (void)hipGetLastError();
+    if (!gt || !valid_width(sym_bytes)) return ANS_E_ARG;
+    if (nchunks && !d_starts) return ANS_E_ARG;
+    HIP_TRY(hipSetDevice(gt->g->device));
+    uint64_t lmax = 0;
+    if (!gt->ts64) {
+        const int rc = device_lmax(d_starts, nchunks, sym_bytes, pick(gt, stream), &lmax);
+        if (rc) return rc;
+    }
     return dev_decode_var(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, seed, d_syms, sym_bytes,
-                          d_status, stream, 0);
+                          d_status, stream, lmax);
 }
 
 int ans_dev_decode_var_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,

@@ -122,6 +122,12 @@ struct FastTable {
     const DecBucketC* dbkt_c;
     uint32_t dec_c;
     uint32_t dec_c_shift;
+    // k_decode kModeU (ans_fast.hpp): the quotient from below without a fix-up; u = head - q_m*norm
+    // in [0, 2 norm) indexes a virtual 512-symbol alphabet whose buckets (width 2^dec_u_shift)
+    // all resolve among three candidates.  dec_u_img is the LDS image (fast::kDecTableBytes).
+    const uint32_t* dec_u_img;
+    uint32_t dec_u;
+    uint32_t dec_u_shift;
 };
 
 }  // namespace shuffle_coding

@@ -182,14 +182,25 @@ def _all_gather_varlen(local, counts, starts, out, group):
         out[starts[r]:starts[r] + counts[r]] = p.cpu().numpy()[:counts[r]].view(np.uint64)
 
 
+def _dtype_of_num(num):
+    """The numpy dtype whose .num is `num` (the integer and float types a decoder returns)."""
+    for t in (np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16, np.int32, np.int64, np.bool_,
+              np.float32, np.float64):
+        if np.dtype(t).num == num:
+            return np.dtype(t)
+    raise ValueError(f"unexpected decoder dtype number {num}")
+
+
 def decode_distributed(decode_shard, data, offsets, lens, n, chunk_len, group=None, dst=0, out=None,
-                       dtype=np.uint8, piece=PIECE):
+                       dtype=None, piece=PIECE):
     """Inverse of encode_distributed: each rank decodes its chunk range of the container
     (decode_shard(data, offsets, lens, n_local, chunk_len) -> symbols; `data` the whole
     container in memory, or a path to it, which each rank maps and reads its range of).
 
     out=None: rank `dst` returns the n symbols, the others None.  out=path: the symbols are
     written there (`dtype` elements), each rank its own range; every rank returns None.
+    dtype=None: the decoders' own dtype (the widest over the ranks that decoded symbols, agreed
+    through one all_gather); a dtype that cannot hold every decoded value raises.
     """
     import torch.distributed as dist
 
@@ -204,9 +215,16 @@ def decode_distributed(decode_shard, data, offsets, lens, n, chunk_len, group=No
             else np.zeros(0, np.uint8)
     else:
         src = np.asarray(data[base:end])
-    local = np.ascontiguousarray(np.asarray(decode_shard(np.asarray(src), off - np.uint64(base), ln, s1 - s0,
-                                                         chunk_len), dtype))
-    w = np.dtype(dtype).itemsize
+    res = np.asarray(decode_shard(np.asarray(src), off - np.uint64(base), ln, s1 - s0, chunk_len))
+    if dtype is None:  # every rank must write the same element width: agree on the decoders' dtype
+        nums = _all_gather_ints([s1 - s0, res.dtype.num], group)
+        found = [_dtype_of_num(int(k)) for m, k in nums if m > 0]
+        dtype = np.result_type(*found) if found else res.dtype
+    dtype = np.dtype(dtype)
+    local = np.ascontiguousarray(res.astype(dtype, copy=False))
+    if res.size and not np.array_equal(local, res):
+        raise ValueError(f"decoded symbols do not fit {dtype} (decoder returned {res.dtype})")
+    w = dtype.itemsize
     if out is not None:
         if rank == dst:
             with open(out, "wb") as f:

@@ -1,0 +1,41 @@
+"""bench.py's launch contract (the driver's `python bench.py --gpus N`, one process per GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def test_gpus_must_match_world_size():
+    # under a launcher, --gpus must equal WORLD_SIZE (refused before any GPU call)
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_launches_two_ranks_itself():
+    """`bench.py --gpus 2` with no launcher starts two ranks (a torch.distributed.run child, no
+    exec) that share the box's one GPU with gloo for the barrier and gather: rank 0's line says
+    n_gpus 2, the value aggregates both shards, and the C4 sub-object reports both ranks."""
+    env = dict(os.environ, BENCH_SHARE_DEVICE="1", BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", BENCH, "--gpus", "2", "--steps", "3", "--warmup", "1", "--log2n", "24",
+           "--c4-log2n", "22", "--no-cpu-baseline", "--no-dense", "--no-host"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == "weak"
+    # whole-job aggregate: both 2^24-symbol shards over the slowest rank's time per step
+    assert abs(d["value"] - 2 * (1 << 24) / (d["ms_per_step"] * 1e-3) / 2**30) < 0.01 * d["value"]
+    assert d["per_rank_ms_per_step"]["max"] == d["ms_per_step"]
+    assert d["c4"]["per_rank"]["ms_per_step"]["max"] == d["c4"]["ms_per_step"]
+    assert d["c4"]["workload"].startswith("C4: 2^22 iid u16 symbols per GPU")

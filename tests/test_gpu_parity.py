@@ -218,7 +218,7 @@ def test_gen_iid_matches_oracle(gpu):
 
 
 # ---------------------------------------------------------------- full-size configs (device-resident)
-def _oracle_slices(masses, seed, n, chunk_len, nslices=64):
+def _oracle_slices(masses, seed, n, chunk_len, nslices=64, start=0):
     """The oracle's streams of the whole workload, chunk-parallel on the host cores: contiguous
     chunk ranges (slices), each generated and encoded on its own thread (ctypes releases the
     GIL).  Returns [(c0, c1)], the lens of every chunk, and per slice the sha256 of its dense
@@ -231,7 +231,7 @@ def _oracle_slices(masses, seed, n, chunk_len, nslices=64):
 
     def work(b):
         a, e = b[0] * chunk_len, min(n, b[1] * chunk_len)
-        syms = orc.gen_iid(masses, seed, a, e - a)
+        syms = orc.gen_iid(masses, seed, start + a, e - a)
         d, _, ln = orc.encode_chunks(masses, syms, chunk_len)
         return ln, hashlib.sha256(d.tobytes()).hexdigest()
 
@@ -240,10 +240,11 @@ def _oracle_slices(masses, seed, n, chunk_len, nslices=64):
     return bounds, np.concatenate([r[0] for r in res]).astype(np.int64), [r[1] for r in res]
 
 
-def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed):
-    """Device-resident encode + decode of the whole workload; EVERY chunk's length and the
-    bytes of the whole compacted stream (sha256 per slice of chunks) must equal the oracle's
-    (src/ans.rs:255-260), and decode must be lossless."""
+def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed, start=0):
+    """Device-resident encode + decode of the whole workload (symbols [start, start + n) of the
+    global array: one bench rank's shard); EVERY chunk's length and the bytes of the whole
+    compacted stream (sha256 per slice of chunks) must equal the oracle's (src/ans.rs:255-260),
+    and decode must be lossless."""
     torch = pytest.importorskip("torch")
     dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[sym_bytes]
     gt = A.GpuTable(gpu, A.Categorical(masses))
@@ -252,7 +253,7 @@ def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed):
     nchunks = -(-n // chunk_len)
     cap = gt.slot_capacity(chunk_len)
     syms = torch.empty(n, dtype=dt, device="cuda")
-    gt.dev_gen_iid(seed, 0, n, syms, sym_bytes, stream)
+    gt.dev_gen_iid(seed, start, n, syms, sym_bytes, stream)
     slots = torch.empty(nchunks * cap, dtype=torch.uint8, device="cuda")
     lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
     status = torch.zeros(1, dtype=torch.int32, device="cuda")
@@ -286,9 +287,9 @@ def _device_roundtrip(gpu, masses, n, chunk_len, sym_bytes, seed):
     dense_h = dense[:total].cpu().numpy()
     del dense
     # the device generator is the oracle's (spot check; the streams below depend on all of it)
-    ref = orc.gen_iid(masses, seed, n - 4096, 4096)
+    ref = orc.gen_iid(masses, seed, start + n - 4096, 4096)
     assert np.array_equal(syms[n - 4096:].cpu().numpy().astype(np.int64) & ((1 << (8 * sym_bytes)) - 1), ref)
-    bounds, olens, ohash = _oracle_slices(masses, seed, n, chunk_len)
+    bounds, olens, ohash = _oracle_slices(masses, seed, n, chunk_len, start=start)
     assert np.array_equal(lens_h, olens), "every chunk's stream length"
     for (c0, c1), h in zip(bounds, ohash):
         a = int(offs_h[c0])
@@ -314,9 +315,12 @@ def test_c3_pow2_norm_bit_exact(gpu):
 
 
 def test_c4_shard_u16_round_trip(gpu):
-    # SURVEY.md §8d C4 table (65,536 symbols, norm 134,561,356); one 2^27-symbol shard, all chunks
-    total = _device_roundtrip(gpu, A.c4_masses(), 1 << 27, 4096, 2, 2)
-    assert 1.9 < total / (1 << 27) < 2.1
+    # SURVEY.md §8d C4 (65,536 symbols, norm 134,561,356): the whole 2^29-symbol shard the bench
+    # codes on each GPU, here rank 7's of 8 (global symbols [7 * 2^29, 8 * 2^29)); all 131,072
+    # chunks' lengths and bytes against the oracle
+    n = 1 << 29
+    total = _device_roundtrip(gpu, A.c4_masses(), n, 4096, 2, 2, start=7 * n)
+    assert 1.9 < total / n < 2.1
 
 
 def test_compact_packs_exact_bytes(gpu):
@@ -666,6 +670,55 @@ def test_var_chunks_bit_exact(gpu, which, multiset_masses):
         got = data[int(offsets[c]):int(offsets[c] + lens[c])].tobytes()
         assert got == want, c
     back = gt.decode_var_chunks(data, offsets, lens, starts, dtype)
+    assert np.array_equal(back, syms.astype(dtype))
+
+
+@pytest.mark.parametrize("which,layout", [("c3", "mixed"), ("c4", "mixed"), ("multiset", "mixed"),
+                                          ("c3", "one_long")])
+def test_var_chunks_device_api_bit_exact(gpu, which, layout, multiset_masses):
+    """ans_dev_encode_var_chunks_ex / ans_dev_decode_var_chunks_ex with device-resident starts:
+    the library finds the longest chunk on the device and stages the chunks for the fast
+    kernels (mixed lengths), or keeps the generic kernels when the padded layout would exceed
+    its budget (one long chunk among a thousand empty ones).  Either way every slot holds the
+    host API's (= the oracle's) stream of its chunk and decoding is lossless."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(47)
+    masses = {"c3": A.c3_masses(), "multiset": multiset_masses, "c4": A.c4_masses()}[which]
+    if layout == "mixed":
+        sizes = np.concatenate([[0, 1, 0, 7], rng.integers(0, 3000, 300), [20000, 0]]).astype(np.uint64)
+    else:
+        sizes = np.concatenate([np.zeros(1000, np.uint64), [200_000], [5]]).astype(np.uint64)
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    n, nchunks = int(starts[-1]), len(sizes)
+    nz = np.flatnonzero(masses)
+    p = masses[nz].astype(np.float64)
+    syms = rng.choice(nz, size=n, p=p / p.sum()).astype(np.uint32)
+    dtype, w = (np.uint16, 2) if len(masses) > 256 else (np.uint8, 1)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    ref, roffs, rlens = gt.encode_var_chunks(syms.astype(dtype), starts)
+    cap = gt.slot_capacity(int(sizes.max()))
+    stream = torch.cuda.Stream()
+    tdt = torch.uint8 if w == 1 else torch.int16
+    d_syms = torch.from_numpy(syms.astype(dtype).view(np.int16) if w == 2 else syms.astype(np.uint8)).to("cuda")
+    d_starts = torch.from_numpy(starts.view(np.int64)).to("cuda")
+    slots = torch.zeros(nchunks * cap, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    s = stream.cuda_stream
+    A._check(A.lib().ans_dev_encode_var_chunks_ex(gt.h, d_syms.data_ptr(), w, nchunks, d_starts.data_ptr(), A.GEN_ZEROS,
+                                                  0, slots.data_ptr(), cap, lens.data_ptr(), status.data_ptr(), s))
+    out = torch.zeros(max(n, 1), dtype=tdt, device="cuda")
+    A._check(A.lib().ans_dev_decode_var_chunks_ex(gt.h, slots.data_ptr(), None, cap, lens.data_ptr(), nchunks,
+                                                  d_starts.data_ptr(), A.GEN_ZEROS, 0, out.data_ptr(), w,
+                                                  status.data_ptr(), s))
+    assert gpu.status(status, stream) == 0
+    lens_h = lens.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(lens_h, rlens)
+    slots_h = slots.cpu().numpy()
+    for c in range(nchunks):
+        got = slots_h[c * cap:c * cap + int(lens_h[c])].tobytes()
+        assert got == ref[int(roffs[c]):int(roffs[c] + rlens[c])].tobytes(), c
+    back = out[:n].cpu().numpy().view(dtype) if w == 2 else out[:n].cpu().numpy()
     assert np.array_equal(back, syms.astype(dtype))
 
 

@@ -56,7 +56,8 @@ def _worker(rank, world, port, masses, syms, chunk_len, q, mode, tmp):
                 with open(path, "rb") as f:
                     data = f.read()
                 q.put(("enc", data, offsets.tolist(), lens.tolist()))
-                q.put(("dec", np.fromfile(sym_path, np.uint8).tolist()))
+                # dtype=None: the file holds the decoder's own elements (the oracle's uint32)
+                q.put(("dec", np.fromfile(sym_path, np.uint32).tolist()))
             return
         # in memory: point-to-point pieces of 1000 bytes into rank 0's preallocated buffers
         got = shards.encode_distributed(enc, syms, chunk_len, piece=1000)
@@ -75,11 +76,13 @@ def _worker(rank, world, port, masses, syms, chunk_len, q, mode, tmp):
 
 
 @pytest.mark.parametrize("mode", ["memory", "file"])
-@pytest.mark.parametrize("n,chunk_len", [(50_000, 4096), (4096 * 5, 4096), (999, 10), (5, 10)])
-def test_two_rank_gloo_matches_single_process(n, chunk_len, mode, tmp_path):
+@pytest.mark.parametrize("n,chunk_len,nsym", [(50_000, 4096, 256), (4096 * 5, 4096, 256), (999, 10, 256), (5, 10, 256),
+                                              (30_000, 4096, 65_536)])
+def test_two_rank_gloo_matches_single_process(n, chunk_len, nsym, mode, tmp_path):
+    # nsym 65,536: symbols above 255 survive the assembly (no cast to an 8-bit default dtype)
     import torch.multiprocessing as mp
 
-    masses = np.asarray([1 + (i * 7919) % 4000 for i in range(256)], np.uint64)
+    masses = np.asarray([1 + (i * 7919) % 4000 for i in range(nsym)], np.uint64)
     syms = orc.gen_iid(masses, 11, 0, n)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -98,6 +101,27 @@ def test_two_rank_gloo_matches_single_process(n, chunk_len, mode, tmp_path):
     assert data == ref_data.tobytes()
     assert offsets == ref_off.tolist() and lens == ref_lens.tolist()
     assert results["dec"][0] == syms.tolist()
+    if nsym > 256:
+        assert max(results["dec"][0]) > 255
+
+
+def test_decode_dtype_that_loses_values_raises():
+    dec = lambda d, o, l, n, L: np.array([3, 300], np.uint32)  # noqa: E731
+
+    import torch.distributed as dist
+    if dist.is_initialized():
+        pytest.skip("a process group is already up")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with pytest.raises(ValueError, match="do not fit"):
+            shards.decode_distributed(dec, np.zeros(4, np.uint8), np.zeros(1, np.uint64), np.full(1, 4, np.uint64),
+                                      2, 10, dtype=np.uint8)
+        got = shards.decode_distributed(dec, np.zeros(4, np.uint8), np.zeros(1, np.uint64), np.full(1, 4, np.uint64),
+                                        2, 10)
+        assert got.dtype == np.uint32 and got.tolist() == [3, 300]
+    finally:
+        dist.destroy_process_group()
 
 
 def _gpu_worker(rank, world, port, masses, syms, chunk_len, q):

@@ -37,7 +37,8 @@ def main():
     dirs = sys.argv[1:3]
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     sync = os.environ.get("AB_NOSYNC") != "1"  # AB_NOSYNC=1: back-to-back launches, no idle gaps
-    masses_fn, log2n, sym_bytes, seed = bench.CONFIGS[os.environ.get("AB_CONFIG", "c3")]
+    masses_name, log2n, sym_bytes, seed = bench.CONFIGS[os.environ.get("AB_CONFIG", "c3")]
+    masses_fn = getattr(A, masses_name)
     log2n = int(os.environ.get("AB_LOG2N", log2n))
     n, L = 1 << log2n, 4096
     torch.cuda.set_device(0)
