@@ -215,6 +215,20 @@ struct RingT {
 };
 using Ring = RingT<kEncRingBase>;
 
+// 8 * byte b of w in one SDWA shift (an LDS row offset straight from a u8 symbol; for byte 0
+// the compiler emitted a shift and a mask).  b is a compile-time constant after unrolling.
+__device__ __forceinline__ uint32_t byte_x8(uint32_t w, int b) {
+    uint32_t r;
+    const uint32_t three = 3;
+    switch (b) {
+    case 0: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(three), "v"(w)); break;
+    case 1: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(three), "v"(w)); break;
+    case 2: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(three), "v"(w)); break;
+    default: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(three), "v"(w)); break;
+    }
+    return r;
+}
+
 template <typename Sym>
 __device__ __forceinline__ uint32_t sym_of(const uint4& v, int j) {
     constexpr int per = 4 / static_cast<int>(sizeof(Sym));
@@ -363,8 +377,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         EncRow e;
         uint64_t thr;
     };
-    auto row = [&](uint32_t s) __attribute__((always_inline)) {
-        const uint32_t off = 8 * s;  // the tables sit at LDS offset 0
+    auto row_at = [&](uint32_t off) __attribute__((always_inline)) {  // off = 8 * symbol (tables at LDS offset 0)
         const uint64_t mc = lds_ld64(off + kEncMcOffset);
         Row r;
         r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
@@ -445,15 +458,16 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto process = [&](const uint4& unit, uint32_t upos) __attribute__((always_inline)) {
         // rows are read one symbol ahead; the scheduling barriers keep the compiler from
         // hoisting all sixteen reads (and their registers) to the top of the unit
-        auto rsym = [&](int j) __attribute__((always_inline)) {
-            return kByteRows ? sym_of<Sym>(unit, j) : min(sym_of<Sym>(unit, j), sentinel);
+        auto roff_rt = [&](const uint4& v, int j) __attribute__((always_inline)) {  // 8 * symbol j of the unit
+            if constexpr (kByteRows) return byte_x8(j == 0 || j == 1 || j == 2 || j == 3 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w, j & 3);
+            else return 8 * min(sym_of<Sym>(v, j), sentinel);
         };
-        Row e_next = row(rsym(U - 1));
+        Row e_next = row_at(roff_rt(unit, U - 1));
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             __builtin_amdgcn_sched_barrier(0);
             const Row e = e_next;
-            if (j > 0) e_next = row(rsym(j - 1));
+            if (j > 0) e_next = row_at(roff_rt(unit, j - 1));
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
             uint32_t k8 = bytes_out_thr8(e.thr);
             if constexpr (kRare) {
@@ -802,7 +816,12 @@ struct DecChain {
         P -= static_cast<int32_t>(renorm_up<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        const uint64_t raw = qest_m1(head, rcp_norm);  // q_m + 0x43300000'00000000
+        // qest_m1 with 1/norm from its SGPR pair (the asm form's "v" operand copied it into a
+        // VGPR pair every step: one v_mov_b64)
+        double hd;
+        asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
+        const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
+        const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(__builtin_fma(xd, rcp_norm, 4503599627370495.0)));  // q_m + 0x43300000'00000000
         cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
         qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
     }

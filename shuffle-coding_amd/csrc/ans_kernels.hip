@@ -708,7 +708,10 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
             constexpr int U = 16 / sizeof(Sym);
 #define DECV(SPP, MODE, P24, J4) fast::k_decode<Sym, SPP, MODE, P24, J4, true><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
 #define DECV_P(SPP, MODE, J4) if (ft.pmax < (1u << 24)) DECV(SPP, MODE, true, J4); else DECV(SPP, MODE, false, J4)
-#define DECV_M(SPP, J4) if (ft.dec_far) { DECV_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DECV_P(SPP, fast::kModeU, J4); } else { DECV_P(SPP, fast::kModeRows, J4); }
+            // the u-domain tables are built for u8 symbols' kernels only (the wider-symbol
+            // instantiations of a <= 256-symbol table keep kModeRows: fewer kernels to compile)
+            constexpr int kU = sizeof(Sym) == 1 ? fast::kModeU : fast::kModeRows;
+#define DECV_M(SPP, J4) if (ft.dec_far) { DECV_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DECV_P(SPP, kU, J4); } else { DECV_P(SPP, fast::kModeRows, J4); }
             // only the combinations a table can select are instantiated: u8 (U = 16) takes
             // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
             constexpr bool kHalf = U * 4 > 60;
@@ -861,7 +864,8 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
 #define DEC(SPP, MODE, P24, J4) fast::k_decode<Sym, SPP, MODE, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
 #define DEC_P(SPP, MODE, J4) if (ft.pmax < (1u << 24)) DEC(SPP, MODE, true, J4); else DEC(SPP, MODE, false, J4)
-#define DEC_M(SPP, J4) if (ft.dec_far) { DEC_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DEC_P(SPP, fast::kModeU, J4); } else { DEC_P(SPP, fast::kModeRows, J4); }
+            constexpr int kU = sizeof(Sym) == 1 ? fast::kModeU : fast::kModeRows;  // (as in launch_staged_decode)
+#define DEC_M(SPP, J4) if (ft.dec_far) { DEC_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DEC_P(SPP, kU, J4); } else { DEC_P(SPP, fast::kModeRows, J4); }
             // only the combinations a table can select are instantiated: u8 (U = 16) takes
             // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
             constexpr bool kHalf = U * 4 > 60;
@@ -1317,19 +1321,6 @@ __global__ __launch_bounds__(1024) void k_scan_lens(const uint32_t* __restrict__
     if (t == 1023) offs[n] = part[1023];
 }
 
-// Like k_expand, with the batch's dense bytes starting at container offset `base`.
-__global__ __launch_bounds__(kBlock) void k_expand_based(const uint8_t* __restrict__ in,
-                                                         const uint64_t* __restrict__ offsets, uint64_t base,
-                                                         const uint32_t* __restrict__ lens, uint64_t nchunks,
-                                                         uint8_t* __restrict__ slots, uint64_t slot_cap) {
-    const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
-    const uint32_t lane = threadIdx.x & 63;
-    if (c >= nchunks) return;
-    const uint8_t* s = in + (offsets[c] - base);
-    uint8_t* d = slots + c * slot_cap;
-    wave_copy(d, s, lens[c], lane);
-}
-
 void pipe_release(HostPipe* p) {
     for (PipeSlot& s : p->slot) {
         (void)hipFree(s.d_syms);
@@ -1401,7 +1392,9 @@ int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks,
         for (PipeSlot& s : p->slot) {
             HIP_TRY(hipMalloc(&s.d_syms, syms + 16));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_slots), slots + 16));
-            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dense), dense + 16));
+            // + 256: the fast decoders read whole aligned 128-B lines around each stream, so
+            // the last stream of a batch may touch the line past its span
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dense), dense + 256));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_lens), sizeof(uint32_t) * chunks + 16));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_offs), sizeof(uint64_t) * (chunks + 1) + 16));
             HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_lens), sizeof(uint32_t) * chunks + 16));
@@ -1513,9 +1506,9 @@ int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_
 }
 
 // Decode a host dense container into host symbols.  Batch b: its byte span and rebased
-// offsets/lengths H2D (s_in) -> expansion into the slot layout and decode (compute stream
-// b & 1) ->
-// symbols D2H (s_out).  No host synchronisation inside the loop beyond staging reuse.
+// offsets/lengths H2D (s_in) -> decode of the span in place (compute stream b & 1; the
+// decoders read a dense container at any alignment, fast::DecChain::start) -> symbols D2H
+// (s_out).  No host synchronisation inside the loop beyond staging reuse.
 // Returns kPipeScattered when some batch's streams spread over more than twice its slot bytes
 // (a container that is not dense); the caller then takes the whole-buffer path.
 template <typename Sym>
@@ -1555,16 +1548,13 @@ int pipe_decode(ans_gpu_table* gt, const uint8_t* in, const uint64_t* offsets, c
             HIP_TRY(hipStreamWaitEvent(p->s_in, s.ev_out, 0));  // its buffers drained
         }
         std::memcpy(s.h_lens, l32 + c0, sizeof(uint32_t) * nc);
-        std::memcpy(s.h_offs, offsets + c0, sizeof(uint64_t) * nc);
+        for (uint64_t j = 0; j < nc; ++j) s.h_offs[j] = offsets[c0 + j] - lo[b];  // into the batch's span
         if (span[b]) HIP_TRY(hipMemcpyAsync(s.d_dense, in + lo[b], span[b], hipMemcpyHostToDevice, p->s_in));
         HIP_TRY(hipMemcpyAsync(s.d_lens, s.h_lens, sizeof(uint32_t) * nc, hipMemcpyHostToDevice, p->s_in));
         HIP_TRY(hipMemcpyAsync(s.d_offs, s.h_offs, sizeof(uint64_t) * nc, hipMemcpyHostToDevice, p->s_in));
         HIP_TRY(hipEventRecord(s.ev_in, p->s_in));
         HIP_TRY(hipStreamWaitEvent(sc, s.ev_in, 0));
-        k_expand_based<<<grid_for(nc * 64), kBlock, 0, sc>>>(s.d_dense, s.d_offs, lo[b], s.d_lens, nc, s.d_slots,
-                                                              slot_cap);
-        HIP_TRY(hipGetLastError());
-        if ((rc = launch_decode<Sym>(gt, s.d_slots, nullptr, slot_cap, s.d_lens, nb, chunk_len, gen_kind, s.d_syms,
+        if ((rc = launch_decode<Sym>(gt, s.d_dense, s.d_offs, slot_cap, s.d_lens, nb, chunk_len, gen_kind, s.d_syms,
                                      p->d_status, sc, fast::ChunkInit{ini.kind, ini.seed + c0})))
             return rc;
         HIP_TRY(hipEventRecord(s.ev_comp, sc));
@@ -2534,9 +2524,9 @@ int ans_gpu_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_l
         if (lens[j] > 0xffffffffull || offsets[j] > in_len || lens[j] > in_len - offsets[j]) return ANS_E_LEN;
         l32[j] = static_cast<uint32_t>(lens[j]);
     }
-    // The container is expanded into the encoder's slot layout on the device, so full chunks
-    // take the fast kernel; slots are widened if a (possibly corrupt) stream is longer than
-    // the worst case of a valid one.
+    // The fast decoders read the container in place (any stream alignment); slot_cap (widened
+    // if a possibly corrupt stream is longer than a valid one can be) sizes the pipeline's
+    // batches and tells a dense container from a scattered one.
     uint64_t slot_cap = 0, max_len = 0;
     ans_gpu_slot_capacity(gt, chunk_len, &slot_cap);
     for (uint64_t j = 0; j < nchunks; ++j) max_len = std::max<uint64_t>(max_len, l32[j]);
@@ -2561,26 +2551,22 @@ int ans_gpu_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_l
         }
         if (rc != kPipeScattered) return rc;
     }
-    // streams scattered over the buffer: one upload of the whole input
+    // streams scattered over the buffer: one upload of the whole input, decoded in place (+256:
+    // the fast decoders read whole aligned 128-B lines around each stream)
     const hipStream_t s = gt->g->stream;
-    DevBuf d_in, d_off, d_lens, d_status, d_out, d_slots;
-    HIP_TRY(d_in.alloc(in_len + 16));
+    DevBuf d_in, d_off, d_lens, d_status, d_out;
+    HIP_TRY(d_in.alloc(in_len + 256));
     HIP_TRY(d_off.alloc(nchunks * sizeof(uint64_t)));
     HIP_TRY(d_lens.alloc(nchunks * sizeof(uint32_t)));
     HIP_TRY(d_status.alloc(sizeof(uint32_t)));
     HIP_TRY(d_out.alloc(n * sym_bytes));
-    HIP_TRY(d_slots.alloc(nchunks * slot_cap));
     if (in_len) HIP_TRY(hipMemcpyAsync(d_in.p, in, in_len, hipMemcpyHostToDevice, s));
     if (nchunks) {
         HIP_TRY(hipMemcpyAsync(d_off.p, offsets, nchunks * sizeof(uint64_t), hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_lens.p, l32.data(), nchunks * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        k_expand<<<grid_for(nchunks * 64), kBlock, 0, s>>>(static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_off.p),
-                                                           static_cast<uint32_t*>(d_lens.p), nchunks,
-                                                           static_cast<uint8_t*>(d_slots.p), slot_cap);
-        HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMemsetAsync(d_status.p, 0, sizeof(uint32_t), s));
-    int rc = ans_dev_decode_chunks_ex(gt, static_cast<uint8_t*>(d_slots.p), nullptr, slot_cap,
+    int rc = ans_dev_decode_chunks_ex(gt, static_cast<uint8_t*>(d_in.p), static_cast<uint64_t*>(d_off.p), slot_cap,
                                       static_cast<uint32_t*>(d_lens.p), n, chunk_len, gen_kind, seed, d_out.p,
                                       sym_bytes, static_cast<uint32_t*>(d_status.p), s);
     if (rc) return rc;
