@@ -1,5 +1,5 @@
 # Builds the library as of a git revision (default HEAD) into shuffle-coding_amd/lib_<name>/,
-# for same-box A/B runs with tools/libab.sh.  usage: bash tools/build_base.sh [rev] [name]
+# for same-box A/B runs with tools/inproc_ab.py or tools/gpu_ab.sh.  usage: bash tools/build_base.sh [rev] [name]
 set -e
 REV=${1:-HEAD}; NAME=${2:-base}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
