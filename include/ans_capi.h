@@ -140,6 +140,7 @@ void ans_gpu_table_free(ans_gpu_table *gt);
 #define ANS_PATH_DEC_WIDE 32u   /* large alphabet: LDS prefix icdf + global buckets */
 #define ANS_PATH_DEC_COMPACT 64u /* ... whose global buckets are 16 B (u16 candidate offsets) */
 #define ANS_PATH_ENC_PACKED 128u /* large-alphabet encoder with the packed (u32 base + u16) LDS prefix */
+#define ANS_PATH_DEC_U 256u     /* LDS decoder without the quotient fix-up (u-domain tables; u8 symbols) */
 int ans_gpu_table_paths(const ans_gpu_table *gt, uint32_t *paths);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);
@@ -206,8 +207,11 @@ int ans_dev_sample_iid(ans_gpu_table *gt, uint64_t seed, uint64_t n, uint64_t ch
 int ans_gpu_sample_iid(ans_gpu_table *gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void *out, int sym_bytes);
 /* Variable-length chunks: chunk c is symbols [starts[c], starts[c+1]) (nchunks + 1
  * non-decreasing entries), still one reference message each, e.g. one graph or one record per
- * chunk.  Generic kernels, one lane per chunk; slot_cap = ans_gpu_slot_capacity of the longest
- * chunk.  Symbols live at their absolute index (the buffers span [0, starts[nchunks])). */
+ * chunk.  One lane per chunk; slot_cap = ans_gpu_slot_capacity of the longest chunk.  Symbols
+ * live at their absolute index (the buffers span [0, starts[nchunks])).  The chunks are staged
+ * for the fast kernels when the padded layout stays within twice the symbols plus 64 MiB (else
+ * the generic kernels); the ans_dev_ entries find the longest chunk on the device, which costs
+ * one 16-byte copy back and a synchronisation of `stream` before the kernels are queued. */
 int ans_dev_encode_var_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, uint64_t nchunks,
                               const uint64_t *d_starts, uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens,
                               uint32_t *d_status, void *stream);

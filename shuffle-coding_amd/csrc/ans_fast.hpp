@@ -446,7 +446,20 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         // the q_m + 1 fix-up never touches 64 bits and needs no sign extension.
         const uint64_t qb = qest_m1(head, e.rcp);  // q_m = qb - 0x43300000'00000000
         const uint32_t rm = lo32(head) - lo32(qb) * e.mass;
-        const uint32_t a = e.cum + rm + (rm >= e.mass ? static_cast<uint32_t>(norm) - e.mass : 0u);
+        // a = cum + (rm < p ? rm : rm - p + norm): the borrow of rm - p (v_sub_co) selects, so
+        // neither norm - p nor a separate compare is formed
+        uint32_t a;
+        {
+            uint32_t t, sel;
+            asm("v_sub_co_u32 %0, vcc, %2, %3\n\t"
+                "v_add_u32 %1, %4, %0\n\t"
+                "s_nop 0\n\t"  // two wait states between the VCC write and its read as a mask
+                "v_cndmask_b32 %1, %1, %2, vcc"
+                : "=&v"(t), "=&v"(sel)
+                : "v"(rm), "v"(e.mass), "s"(static_cast<uint32_t>(norm))
+                : "vcc");
+            a = e.cum + sel;
+        }
         // the high word as v_mul_lo_u32 + v_add3 on the raw exponent word (its 0x43300000 * norm
         // comes off as a scalar): a second v_mad_u64_u32 costs two v_mov and the exponent a v_add
         const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * static_cast<uint32_t>(norm) + a;
@@ -472,8 +485,11 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             uint32_t k8 = bytes_out_thr8(e.thr);
             if constexpr (kRare) {
                 EncRow r = e.e;
-                const bool rare = static_cast<int32_t>(hi32(static_cast<uint64_t>(__double_as_longlong(r.rcp)))) < 0;
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
+                const uint32_t rh = hi32(static_cast<uint64_t>(__double_as_longlong(r.rcp)));
+                const bool rare = static_cast<int32_t>(rh) < 0;
+                uint64_t any_rare;  // a 32-bit compare of the sign word (the compiler widened it to 64)
+                asm volatile("v_cmp_gt_i32_e64 %0, 0, %1" : "=s"(any_rare) : "v"(rh));
+                if (__builtin_expect(any_rare != 0, 0)) {
                     if (rare) {
                         k8 = (head >> (8 * (KMAX - 1))) > e.thr ? 8u * KMAX : k8;
                         minmass = min(minmass, r.mass);

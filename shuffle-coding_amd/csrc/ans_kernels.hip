@@ -2058,6 +2058,7 @@ int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
     if (ft.usable && ft.dec_wide) p |= ANS_PATH_DEC_WIDE;
     if (ft.usable && ft.dec_wide && ft.dec_c) p |= ANS_PATH_DEC_COMPACT;
     if (ft.usable && ft.enc_wide && ft.enc_pack) p |= ANS_PATH_ENC_PACKED;
+    if (ft.usable && ft.dec_usable && !ft.dec_far && ft.dec_u) p |= ANS_PATH_DEC_U;
     *paths = p;
     return ANS_OK;
 }

@@ -95,6 +95,38 @@ def test_random_tables_bit_exact(gpu, nsym, lo, hi, zero_frac, chunk_len, n):
         _roundtrip_vs_oracle(gpu, masses, syms, chunk_len, dtype)
 
 
+@pytest.mark.parametrize("which", ["c3", "c3p2", "wide_masses", "zeros", "top_of_range", "tiny_masses"])
+def test_u_domain_decoder_bit_exact(gpu, which):
+    """The fix-up-free decoder (ans_fast.hpp kModeU: u = head - q_m * norm in [0, 2 norm) over a
+    512-symbol virtual alphabet) on 256-symbol tables across the fast range: every chunk's bytes
+    equal the oracle's and decoding is lossless; the tables expected to build u-domain buckets
+    report ANS_PATH_DEC_U (a table whose buckets would need a fourth candidate keeps the r02
+    rows, also bit-exact)."""
+    rng = np.random.default_rng(sum(map(ord, which)))
+    if which == "c3":
+        masses = A.c3_masses()
+    elif which == "c3p2":
+        masses = A.c3_pow2_masses()
+    elif which == "wide_masses":
+        masses = rng.integers(1, 1 << 20, 256).astype(np.uint64)
+    elif which == "zeros":
+        masses = rng.integers(1, 1 << 18, 256).astype(np.uint64)
+        masses[rng.choice(256, 60, replace=False)] = 0
+    elif which == "top_of_range":  # norm just below 2^31
+        masses = rng.integers(1 << 21, 1 << 23, 256).astype(np.uint64)
+        masses = (masses * ((1 << 31) - 1) // int(masses.sum())).astype(np.uint64)
+        masses[masses == 0] = 1
+    else:  # masses of a few units beside large ones: kmax 4, half-unit points
+        masses = np.concatenate([rng.integers(1, 4, 16), rng.integers(1 << 12, 1 << 16, 240)]).astype(np.uint64)
+    assert int(masses.sum()) < (1 << 31)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    if which in ("c3", "c3p2"):  # (random tables may hold crowded buckets: then kModeFar / kModeRows)
+        assert gt.paths() & A.ANS_PATH_DEC_U, hex(gt.paths())
+    n = 300 * 4096 + 777
+    syms = orc.gen_iid(masses, 5, 0, n)
+    _roundtrip_vs_oracle(gpu, masses, syms, 4096, np.uint8)
+
+
 @pytest.mark.parametrize("seed", [0, 1])
 def test_fast_decoder_crowded_buckets(gpu, seed):
     """Hundreds of cdf boundaries inside one decode bucket (the bucket table resolves four;
