@@ -142,6 +142,19 @@ __device__ __forceinline__ uint64_t qest_m1(uint64_t x, double rcp) {
     return static_cast<uint64_t>(__double_as_longlong(t));  // raw bits: qest - 1 + 0x43300000'00000000
 }
 
+// round(x / d - 1/2) from the magic constant 2^52 - 1/2 (exact in f64), for x / d >= 1: the
+// estimate's error is below 2^-52 x/d + 2^-48 (<= 2^-4 for x/d < 2^48), so this is floor(x / d)
+// unless x / d lies within that error of an integer, and floor - 1 or floor + 1 there.  Raw bits:
+// the estimate + 0x43300000'00000000.
+__device__ __forceinline__ uint64_t qest_half(uint64_t x, double rcp) {
+    double hd;
+    asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(x)));
+    const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(x)));
+    double t;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "v"(xd), "v"(rcp), "v"(4503599627370495.5));
+    return static_cast<uint64_t>(__double_as_longlong(t));
+}
+
 // TailGenerator::Random (src/ans.rs:129-164): rand_pcg 0.3.1 Pcg64Mcg (MCG-128, XSL-RR-64
 // output) seeded by rand_core 0.6 seed_from_u64 (PCG32 expansion), one byte per draw
 // (rand 0.8.5 Standard<u8> = next_u32() as u8 = next_u64() as u8).  The same restatement as
@@ -397,7 +410,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     const uint64_t norm = t.norm;
     const uint64_t K = t.K;
     const uint32_t sentinel = t.enc_rows - 1;  // zero-mass row: out-of-range symbols land here
-    const uint32_t exp_norm = 0x43300000u * static_cast<uint32_t>(t.norm);  // qest_m1's exponent word x norm
+    const uint32_t exp_norm = 0x43300000u * static_cast<uint32_t>(t.norm);  // the estimate's exponent word x norm
 
     uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
     Funnel f{0, 0, 0, ring.col, ring.col};
@@ -440,26 +453,23 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         f.push(lo32(head), k8);
         head >>= k8;
         // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
-        // (src/ans.rs:103-104, src/codec.rs:64).  With the estimate q_m in {q - 1, q} (head >= p*K
-        // >= p after the renorm, so q >= 1) and r_m = head - q_m*p in [0, 2p):
-        // head = norm*q_m + (cum + r_m + [r_m >= p]*(norm - p)), an addend in [0, 2 norm), so
-        // the q_m + 1 fix-up never touches 64 bits and needs no sign extension.
-        const uint64_t qb = qest_m1(head, e.rcp);  // q_m = qb - 0x43300000'00000000
-        const uint32_t rm = lo32(head) - lo32(qb) * e.mass;
-        // a = cum + (rm < p ? rm : rm - p + norm): the borrow of rm - p (v_sub_co) selects, so
-        // neither norm - p nor a separate compare is formed
-        uint32_t a;
-        {
-            uint32_t t, sel;
-            asm("v_sub_co_u32 %0, vcc, %2, %3\n\t"
-                "v_add_u32 %1, %4, %0\n\t"
-                "s_nop 0\n\t"  // two wait states between the VCC write and its read as a mask
-                "v_cndmask_b32 %1, %1, %2, vcc"
-                : "=&v"(t), "=&v"(sel)
-                : "v"(rm), "v"(e.mass), "s"(static_cast<uint32_t>(norm))
-                : "vcc");
-            a = e.cum + sel;
+        // (src/ans.rs:103-104, src/codec.rs:64).  The estimate round(head/p - 1/2) is q except
+        // where head/p lies within 2^-4 of an integer (C3: head/p < 2^37, so within 2^-15, about
+        // one symbol in 2^14): r = head - q_est*p in 32 bits is then < p exactly when q_est = q,
+        // and the rare lanes where it is not take the exact 64-bit remainder on a voted branch
+        // (q_est = q - 1 or q + 1).  The common path is one compare and one add, where the
+        // estimate from below (q_m in {q - 1, q}) needed a borrow-select on every symbol.
+        uint64_t qb = qest_half(head, e.rcp);  // q_est + 0x43300000'00000000
+        uint32_t rm = lo32(head) - lo32(qb) * e.mass;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= e.mass) != 0, 0)) {
+            if (rm >= e.mass) {
+                const int64_t r = static_cast<int64_t>(head - (qb - 0x4330000000000000ull) * e.mass);
+                const int64_t d = r < 0 ? -1 : 1;
+                qb += static_cast<uint64_t>(d);
+                rm = static_cast<uint32_t>(r - d * static_cast<int64_t>(e.mass));
+            }
         }
+        const uint32_t a = e.cum + rm;
         // the high word as v_mul_lo_u32 + v_add3 on the raw exponent word (its 0x43300000 * norm
         // comes off as a scalar): a second v_mad_u64_u32 costs two v_mov and the exponent a v_add
         const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * static_cast<uint32_t>(norm) + a;
@@ -753,8 +763,11 @@ struct DecChain {
     // Pairs below 0 come from a zero pair in global memory: the same loads, where a register
     // zero-fill cost a point's worth of v_mov on every wave with one lane at its stream start
     // (global address space: a flat load would also count in lgkmcnt and stall the LDS waits)
+    // Positions count from the stream's first byte (src), at any alignment: a pair below the
+    // top one lies wholly inside the stream, so its 16-B loads (unaligned in a dense container;
+    // the hardware runs in unaligned mode) touch only the stream's own bytes.
     __device__ __forceinline__ void fetch_pair(int32_t m) {
-        typedef __attribute__((address_space(1))) const v4u32 gv4;
+        typedef __attribute__((address_space(1), aligned(1))) const v4u32 gv4;
         const uint4* g = m >= 0 ? reinterpret_cast<const uint4*>(src + 128ll * m) : kZeroPage;
         const gv4* gg = reinterpret_cast<const gv4*>(reinterpret_cast<uintptr_t>(g));
 #pragma unroll
@@ -762,6 +775,23 @@ struct DecChain {
             const v4u32 v = gg[k];
             Q[k] = make_uint4(v.x, v.y, v.z, v.w);
         }
+    }
+    // the top pair m (once per stream) may reach past the stream's end, where a wide load could
+    // cross into an unmapped page: it is read as the aligned dwords holding stream bytes (each
+    // inside its 128-B line) and funnelled to the stream's byte alignment by v_alignbyte
+    __device__ __forceinline__ void fetch_top(int32_t m, int32_t len) {
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src) + 128ll * m;
+        const gu32* d0 = reinterpret_cast<const gu32*>(a & ~uintptr_t(3));
+        const uint32_t b = static_cast<uint32_t>(a & 3u);
+        const int32_t last = static_cast<int32_t>(((reinterpret_cast<uintptr_t>(src) + len - 1) >> 2) - (a >> 2));
+        uint32_t d[33];
+#pragma unroll
+        for (int q = 0; q < 33; ++q) d[q] = q <= last ? d0[q] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            Q[k] = make_uint4(ab(d[4 * k + 1], d[4 * k], b), ab(d[4 * k + 2], d[4 * k + 1], b),
+                              ab(d[4 * k + 3], d[4 * k + 2], b), ab(d[4 * k + 4], d[4 * k + 3], b));
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
     // ring base in the ds offsets the row address is one v_and_or of (P << 10) and the lane's column.
@@ -774,16 +804,19 @@ struct DecChain {
     // (v_alignbyte_b32 reads only the low two bits of its shift operand: P needs no mask)
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
     // the top two pages land before decoding starts; the pair below them is requested.
-    // s: the stream's first byte, at any alignment (a dense container).  Positions count from
-    // the 128-B line holding it (base = s - sh), so every fetch is whole aligned lines, read
-    // only from lines that hold stream bytes; the sh bytes below the stream (another chunk's)
-    // are reached only by a corrupt stream, which the final position check reports.
+    // s: the stream's first byte, at any alignment (a dense container).  Positions count from s
+    // itself (sh = 0), so every lane's pages start at its own stream's start: streams of similar
+    // length then cross page boundaries at nearly the same symbols, in a dense container as in
+    // slots, and a wave runs the landing code about once per page rather than at every point
+    // (with pages at absolute 64-B boundaries the packed streams' random phases put some lane's
+    // landing at nearly every point: +2.2 VALU per symbol, profiles/r03_pmc_dense_vs_slot.txt).
     __device__ __forceinline__ void start(const uint8_t* s, int32_t slen) {
-        sh = static_cast<int32_t>(reinterpret_cast<uintptr_t>(s) & 127u);
-        src = s - sh;
-        const int32_t len = slen + sh;
+        sh = 0;
+        src = s;
+        const int32_t len = slen;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
-        fetch_pair(len > 0 ? top >> 1 : -1);
+        if (len > 0) fetch_top(top >> 1, len);
+        else fetch_pair(-1);
         wait_vm();
         put_page(top);
         if (top & 1) {
@@ -827,17 +860,21 @@ struct DecChain {
     // phase 1 for kModeU: the quotient from below, q_m = qq's low word and hi = hi32(q_m) (no
     // fix-up: u = head - q_m * norm in [0, 2 norm) goes to the u-domain tables as it is)
     template <bool kJ4>
-    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
+    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double magic_m1) {
         form_window();
         P -= static_cast<int32_t>(renorm_up<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        // qest_m1 with 1/norm from its SGPR pair (the asm form's "v" operand copied it into a
-        // VGPR pair every step: one v_mov_b64)
+        // qest_m1 with 1/norm from its SGPR pair (an asm "v" operand copied it into a VGPR pair
+        // every step) and the magic 2^52 - 1 from a loop-invariant VGPR pair as the third
+        // operand of one VOP3 v_fma_f64 (__builtin_fma became v_fmac_f64 on a v_mov_b64 copy of
+        // the magic: one 64-bit move per step)
         double hd;
         asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
         const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
-        const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(__builtin_fma(xd, rcp_norm, 4503599627370495.0)));  // q_m + 0x43300000'00000000
+        double tq;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(xd), "s"(rcp_norm), "v"(magic_m1));
+        const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(tq));  // q_m + 0x43300000'00000000
         cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
         qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
     }
@@ -980,6 +1017,9 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t hL8 = renorm_screen(L);
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;
+    // 2^52 - 1 in a VGPR pair for the whole kernel (opaque, so it is not rematerialised per step)
+    double magic_m1;
+    asm("" : "=v"(magic_m1) : "0"(4503599627370495.0));
     const uint32_t shift = kMode == kModeU ? t.dec_u_shift : t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
@@ -1023,7 +1063,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                     __builtin_amdgcn_sched_barrier(0);
                     if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
                     if constexpr (kMode == kModeU) {
-                        ch.template renorm_div_u<kJ4>(L, hL8, norm, rcp_norm);
+                        ch.template renorm_div_u<kJ4>(L, hL8, norm, rcp_norm, magic_m1);
                         ch.lookup_u(shift);
                     } else {
                         ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);

@@ -1,14 +1,19 @@
-# Same-box A/B of two library builds (tools/inproc_ab.py) on C3 and C4, then the GPU test
-# suite, the default bench line and one PMC pass (instruction counts) of the C3 kernels.
+# Same-box A/B of two library builds (tools/inproc_ab.py) on C3, C4 and the C3 dense container;
+# then B becomes the in-tree library on the box (a scratch copy) and the GPU test suite and the
+# default bench line run on it (tools/gpu_step.sh).
 # usage: bash tools/gpu_ab.sh <libdir A> <libdir B>      (libdirs under shuffle-coding_amd/)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u tools/inproc_ab.py $1 $2 40 > gpurun_out/ab_c3.txt 2>&1
-rc=$?; echo "ab c3 rc=$rc"; cat gpurun_out/ab_c3.txt | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
-AB_CONFIG=c4 timeout -k 10 300 python -u tools/inproc_ab.py $1 $2 20 > gpurun_out/ab_c4.txt 2>&1
-rc=$?; echo "ab c4 rc=$rc"; cat gpurun_out/ab_c4.txt | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
+run() {  # tag, env..., iters
+    local tag=$1; shift
+    env "$@" timeout -k 10 300 python -u tools/inproc_ab.py $A $B ${ITERS:-40} > gpurun_out/ab_$tag.txt 2>&1
+    local rc=$?; echo "ab $tag rc=$rc"; grep -v amdgpu.ids gpurun_out/ab_$tag.txt; return $rc
+}
+A=$1; B=$2
+run c3 AB_CONFIG=c3 || exit $?
+ITERS=20 run c4 AB_CONFIG=c4 || exit $?
+run dense AB_CONFIG=c3 AB_DENSE=1 || exit $?
+if [ "$B" != lib ]; then cp shuffle-coding_amd/$B/libshufflecoding_amd.so shuffle-coding_amd/lib/; fi
 bash tools/gpu_step.sh || exit $?
-timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d gpurun_out/pmc_ab -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-c4 --no-host --no-dense > gpurun_out/pmc_ab.log 2>&1
-rc=$?; echo "pmc rc=$rc"; exit $rc

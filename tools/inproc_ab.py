@@ -2,6 +2,7 @@
 
 usage: python tools/inproc_ab.py <libdir A> <libdir B> [iters]
   AB_CONFIG=c4 AB_LOG2N=29: another bench config / size (default: C3 at its full size)
+  AB_DENSE=1: the dense container (ans_dev_encode_dense, decode in place) instead of slots
   libdir: a directory under shuffle-coding_amd/ holding libshufflecoding_amd.so ("lib" = default)
 
 Both builds are loaded side by side (RTLD_LOCAL, each registers its own code object) and run
@@ -39,6 +40,7 @@ def main():
     sync = os.environ.get("AB_NOSYNC") != "1"  # AB_NOSYNC=1: back-to-back launches, no idle gaps
     masses_name, log2n, sym_bytes, seed = bench.CONFIGS[os.environ.get("AB_CONFIG", "c3")]
     masses_fn = getattr(A, masses_name)
+    dense = os.environ.get("AB_DENSE") == "1"
     log2n = int(os.environ.get("AB_LOG2N", log2n))
     n, L = 1 << log2n, 4096
     torch.cuda.set_device(0)
@@ -59,15 +61,24 @@ def main():
                            slots=torch.empty(nch * cap, dtype=torch.uint8, device="cuda"),
                            lens=torch.zeros(nch, dtype=torch.int32, device="cuda"),
                            status=torch.zeros(1, dtype=torch.int32, device="cuda"),
-                           out=torch.empty_like(syms)))
+                           out=torch.empty_like(syms),
+                           offs=torch.empty(A.dense_offsets_entries(nch), dtype=torch.int64, device="cuda"),
+                           dense=torch.empty(nch * cap, dtype=torch.uint8, device="cuda") if dense else None))
 
     def step(i, ev):
         A._lib = libs[i]
         s = setups[i]
         ev[0].record(stream)
-        s["gt"].dev_encode(syms, sym_bytes, n, L, s["slots"], s["cap"], s["lens"], s["status"], stream)
+        if dense:
+            s["gt"].dev_encode_dense(syms, sym_bytes, n, L, s["slots"], s["cap"], s["lens"], s["offs"], s["dense"],
+                                     s["status"], stream)
+        else:
+            s["gt"].dev_encode(syms, sym_bytes, n, L, s["slots"], s["cap"], s["lens"], s["status"], stream)
         ev[1].record(stream)
-        s["gt"].dev_decode(s["slots"], None, s["cap"], s["lens"], n, L, s["out"], sym_bytes, s["status"], stream)
+        if dense:
+            s["gt"].dev_decode(s["dense"], s["offs"], s["cap"], s["lens"], n, L, s["out"], sym_bytes, s["status"], stream)
+        else:
+            s["gt"].dev_decode(s["slots"], None, s["cap"], s["lens"], n, L, s["out"], sym_bytes, s["status"], stream)
         ev[2].record(stream)
 
     for _ in range(3):
@@ -87,6 +98,7 @@ def main():
         s = setups[i]
         if os.environ.get("AB_NOCHECK") != "1":
             assert torch.equal(s["out"], syms), f"{dirs[i]}: round trip differs"
+            assert int(s["status"].item()) == 0, f"{dirs[i]}: device status {int(s['status'].item())}"
         enc = np.median([e[0].elapsed_time(e[1]) for e in evs[i]])
         dec = np.median([e[1].elapsed_time(e[2]) for e in evs[i]])
         print(f"{dirs[i]:10s} enc {enc:.4f} dec {dec:.4f} ms (median of {iters}{'' if sync else ', no sync'})")
