@@ -142,12 +142,19 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         }
     };
     // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
+    // From bit lengths: with d = bitlen(head) - bitlen(pK) >= 0 (head >= norm*K >= pK before a
+    // push), every j with 8j < d holds and every j with 8j > d fails, so k = m - 1 + [(head >> 8m)
+    // >= pK] for m = ceil(d / 8): one 64-bit shift and compare where testing each j took KMAX
+    // (8m <= 40: pK >= K >= 2^25 in the fast range, so d <= 39).  head >= 2^55 here, so its
+    // high word is never zero.
     auto bytes_out8 = [&](uint64_t pK) __attribute__((always_inline)) {
-        uint32_t k = (head >> 8) >= pK ? 8u : 0u;
-        if constexpr (KMAX >= 2) k += (head >> 16) >= pK ? 8u : 0u;
-        if constexpr (KMAX >= 3) k += (head >> 24) >= pK ? 8u : 0u;
-        if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 8u : 0u;
-        return k;
+        uint32_t fh, fp0, fp1;
+        asm("v_ffbh_u32 %0, %1" : "=v"(fh) : "v"(hi32(head)));
+        asm("v_ffbh_u32 %0, %1" : "=v"(fp1) : "v"(hi32(pK)));
+        asm("v_ffbh_u32 %0, %1" : "=v"(fp0) : "v"(lo32(pK)));
+        const uint32_t clz_pk = umin(fp1, fp0 + 32u);  // ffbh(0) = ~0: the low word's count then wins
+        const uint32_t m8 = (clz_pk - fh + 7u) & ~7u;  // 8 * ceil(d / 8)
+        return (head >> m8) >= pK ? m8 : m8 - 8u;
     };
     auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, uint32_t upos) __attribute__((always_inline)) {
 #pragma unroll
