@@ -63,13 +63,19 @@ static_assert(kDecRowOff + 8 * 257 <= kDecTableBytes, "row decode tables fit");
 // the fix-up-free decoder's LDS layout (k_decode kMode = kModeU, FastTable::dec_u): the quotient
 // from below (q_m in {q - 1, q}) leaves u = head - q_m * norm in [0, 2 norm), which indexes a
 // virtual alphabet of 512 symbols: v < 256 is symbol v at cdf(v) (q = q_m), v >= 256 symbol
-// v - 256 at norm + cdf(v - 256) (q = q_m + 1).  Buckets of u as (cdfv(s0+1), cdfv(s0+2))
-// pairs, their u16 s0 values, then 512 rows (cum_row, p) with head = p * q_m + (u - cum_row).
-constexpr uint32_t kDecUNbMax = (kDecTableBytes - 8 * 512) / 10;
-constexpr uint32_t kDecUS0Off = 8 * kDecUNbMax;
-constexpr uint32_t kDecURowOff = (kDecUS0Off + 2 * kDecUNbMax + 15) & ~15u;
+// v - 256 at norm + cdf(v - 256) (q = q_m + 1).  Buckets of u (width 2^us) as 8-B threshold
+// pairs, then 512 rows (cum_row, p) with head = p * q_m + (u - cum_row).  A bucket at a = j << us
+// holds, for its boundaries c = cdfv(s0+1) and cdfv(s0+2) (s0 = the virtual symbol at a), the
+// word ((min(c - a, 2^us) - 1) << (32 - us)) | s0: u's offset in the bucket shifted to the top,
+// rx = u << (32 - us), exceeds it exactly when u >= c (its low bits are zero, the word's are
+// s0), so s = s0 + [rx > w1] + [rx > w2] comes from two compares and two v_addc on w1 itself,
+// with no separate s0 array (one random LDS read fewer per symbol).  The bits of w1 above s0
+// start at bit 32 - us >= 13 and leave the row address ((s << 3) mod 2^16) alone: us <= 19.
+constexpr uint32_t kDecUNbMax = (kDecTableBytes - 8 * 512) / 8;
+constexpr uint32_t kDecURowOff = 8 * kDecUNbMax;
+constexpr uint32_t kDecUShiftMax = 19;
 static_assert(kDecURowOff + 8 * 512 <= kDecTableBytes, "u-domain decode tables fit");
-static_assert(kDecUS0Off + 2 * kDecUNbMax <= 65535 && kDecURowOff <= 65535, "ds offsets");
+static_assert(kDecURowOff <= 65535, "ds offsets");
 // decode lookup modes (k_decode kMode)
 constexpr int kModeFar = 0;   // 16-B buckets, three candidates, voted scan of the staged cdf
 constexpr int kModeRows = 1;  // 8-B buckets, two boundaries, then the symbol's (cdf, pmf) row
@@ -878,23 +884,24 @@ struct DecChain {
         cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
         qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
     }
-    // the u-domain icdf: bucket u >> shift -> (cdfv(s0+1), cdfv(s0+2)) and s0 (u16), the virtual
-    // symbol v = s0 + [u >= cdfv(s0+1)] + [u >= cdfv(s0+2)], then its row (cum_row, p)
-    __device__ __forceinline__ void lookup_u(uint32_t shift) {
+    // the u-domain icdf: bucket u >> shift -> threshold words (w1, w2) with s0 in w1's low bits
+    // (kDecUNbMax), the virtual symbol v = s0 + [rx > w1] + [rx > w2] for rx = u << rshift, then
+    // its row (cum_row, p); only v's low 13 bits reach the row address
+    __device__ __forceinline__ void lookup_u(uint32_t shift, uint32_t rshift) {
         const uint32_t bi = cf >> shift;
         const uint64_t cc = lds_ld64(shl16<3>(bi));  // bi < kDecUNbMax
-        const uint32_t s0 = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(shl16<1>(bi) + kDecUS0Off));
+        const uint32_t rx = cf << rshift;
         asm volatile(
-            "v_cmp_ge_u32 vcc, %[cf], %[c1]\n\t"
+            "v_cmp_gt_u32 vcc, %[rx], %[w1]\n\t"
             "s_nop 1\n\t"
-            "v_addc_co_u32 %[sx], vcc, 0, %[s0], vcc\n\t"
-            "v_cmp_ge_u32 vcc, %[cf], %[c2]\n\t"
+            "v_addc_co_u32 %[sx], vcc, 0, %[w1], vcc\n\t"
+            "v_cmp_gt_u32 vcc, %[rx], %[w2]\n\t"
             "s_nop 1\n\t"
             "v_addc_co_u32 %[sx], vcc, 0, %[sx], vcc"
             : [sx] "=&v"(sx)
-            : [cf] "v"(cf), [c1] "v"(lo32(cc)), [c2] "v"(hi32(cc)), [s0] "v"(s0)
+            : [rx] "v"(rx), [w1] "v"(lo32(cc)), [w2] "v"(hi32(cc))
             : "vcc");
-        const uint64_t row = lds_ld64(kDecURowOff + shl16<3>(sx));  // sx < 512
+        const uint64_t row = lds_ld64(kDecURowOff + shl16<3>(sx));  // (sx mod 2^13) < 512
         cum = lo32(row);
         nxt = hi32(row);  // pmf(s)
         far = false;
@@ -1064,7 +1071,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                     if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
                     if constexpr (kMode == kModeU) {
                         ch.template renorm_div_u<kJ4>(L, hL8, norm, rcp_norm, magic_m1);
-                        ch.lookup_u(shift);
+                        ch.lookup_u(shift, 32u - shift);
                     } else {
                         ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
                         if constexpr (kFar) {

@@ -322,15 +322,19 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         while (((n2 - 1) >> us) + 1 > fast::kDecUNbMax) ++us;
         const uint32_t nbu = static_cast<uint32_t>(((n2 - 1) >> us) + 1);
         uimg.assign(fast::kDecTableBytes, 0);
-        bool ok = true;
+        bool ok = us <= fast::kDecUShiftMax;  // (norm < 3072 * 2^18: s0 below the threshold bits)
+        // threshold word of boundary c in the bucket at a, with s0 in its low bits (ans_fast.hpp
+        // kDecUNbMax): u >= c  <=>  (u - a) << (32 - us) > this word, for u in the bucket
+        auto word = [&](uint64_t a, uint64_t c, uint32_t s0) {
+            const uint64_t rel = std::min<uint64_t>(c - a, 1ull << us);  // >= 1: c > a
+            return static_cast<uint32_t>(((rel - 1) << (32 - us)) | s0);
+        };
         for (uint32_t j = 0; j < nbu && ok; ++j) {
             const uint64_t a = static_cast<uint64_t>(j) << us, end = std::min<uint64_t>(n2, a + (1ull << us));
             const uint32_t s0 = icdfv(a);
             if (cdfv(s0 + 3) < end) ok = false;
-            const uint32_t c12[2] = {static_cast<uint32_t>(cdfv(s0 + 1)), static_cast<uint32_t>(cdfv(s0 + 2))};
-            const uint16_t s16 = static_cast<uint16_t>(s0);
-            std::memcpy(uimg.data() + 8 * j, c12, 8);
-            std::memcpy(uimg.data() + fast::kDecUS0Off + 2 * j, &s16, 2);
+            const uint32_t w12[2] = {word(a, cdfv(s0 + 1), s0), word(a, cdfv(s0 + 2), s0)};
+            std::memcpy(uimg.data() + 8 * j, w12, 8);
         }
         for (uint32_t v = 0; v < 512 && ok; ++v) {
             const uint32_t sv = v & 255u;
