@@ -17,9 +17,11 @@ using namespace shuffle_coding;
 // batch b and the D2H copy of batch b-1 overlap.  Kernels alternate between
 // two compute streams (the context's and s_comp2): a batch's kernels occupy few CUs for about
 // one chain latency (~1 ms for 4096-symbol chunks), so consecutive batches must overlap too.
-// Four streams in all, the per-process hardware queue count.  The workspace persists in the
-// context and grows on demand.
-constexpr int kPipeDepth = 3;
+// The three pipeline streams each get a hardware queue of their own (CU-masked queues are
+// never shared; ans_kernels.hip own_queue_stream).  The workspace persists in the context and
+// grows on demand.
+constexpr int kPipeDepthMax = 8;  // workspace slots: ANS_PIPE_DEPTH (default kPipeDepth) at creation
+constexpr int kPipeDepth = 6;
 struct PipeSlot {
     void* d_syms = nullptr;     // batch symbols
     uint8_t* d_slots = nullptr; // batch streams in the slot layout
@@ -33,7 +35,8 @@ struct PipeSlot {
 };
 struct HostPipe {
     hipStream_t s_in = nullptr, s_out = nullptr, s_comp2 = nullptr;
-    PipeSlot slot[kPipeDepth];
+    PipeSlot slot[kPipeDepthMax];
+    int depth = kPipeDepth;  // slots in use
     uint32_t* d_status = nullptr;
     size_t cap_syms = 0, cap_slots = 0, cap_dense = 0, cap_chunks = 0;  // per slot
     // page-locked callers (device-driven copies): per-call chunk metadata and the carry

@@ -66,7 +66,12 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8
 // v_alignbyte at a wave-uniform dword step and byte shift.  The first and last blocks may hold
 // a neighbouring stream's bytes: those are written byte by byte (no store touches a byte
 // outside the stream, so neighbouring waves never race).  Only source blocks holding stream
-// bytes are read.
+// bytes are read, each once: block j-1 comes from the lane below (DPP wave_shr:1), and for lane
+// 0 from lane 63 of the previous pass (v_readlane), where a second load per lane read every
+// block twice through the L1 (the pack ran at 5.2 TB/s, profiles/r03b_kernel_stats_c3.csv).
+__device__ __forceinline__ uint32_t from_lane_below(uint32_t v, uint32_t carry) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(carry), static_cast<int>(v), 0x138, 0xF, 0xF, false));
+}
 __device__ __forceinline__ void wave_pack(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
                                           uint32_t lane) {
     if (len == 0) return;
@@ -76,9 +81,15 @@ __device__ __forceinline__ void wave_pack(uint8_t* __restrict__ dst, const uint8
     const uint32_t nblk = (dsh + len + 15) / 16;
     const uint32_t bs = (16u - dsh) & 3u;         // byte shift inside the 32-B window
     const uint32_t i0 = (16u - dsh) >> 2;         // first window dword of an output block
-    for (uint32_t j = lane; j < nblk; j += 64) {
-        const uint4 a = j > 0 ? s16[j - 1] : make_uint4(0, 0, 0, 0);
-        const uint4 b = 16 * j < len ? s16[j] : make_uint4(0, 0, 0, 0);  // only blocks holding stream bytes
+    uint4 carry = make_uint4(0, 0, 0, 0);         // block j0 - 1 (none before the stream)
+    for (uint32_t j0 = 0; j0 < nblk; j0 += 64) {  // (wave-uniform: every lane takes part in the DPP moves)
+        const uint32_t j = j0 + lane;
+        const uint4 b = (j < nblk && 16 * j < len) ? s16[j] : make_uint4(0, 0, 0, 0);  // only blocks holding stream bytes
+        const uint4 a = make_uint4(from_lane_below(b.x, carry.x), from_lane_below(b.y, carry.y),
+                                   from_lane_below(b.z, carry.z), from_lane_below(b.w, carry.w));
+        carry = make_uint4(__builtin_amdgcn_readlane(b.x, 63), __builtin_amdgcn_readlane(b.y, 63),
+                           __builtin_amdgcn_readlane(b.z, 63), __builtin_amdgcn_readlane(b.w, 63));
+        if (j >= nblk) continue;
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint32_t o[4];
         // i0 is wave-uniform: a scalar branch picks constant register indices
@@ -553,8 +564,17 @@ __global__ __launch_bounds__(1024) void k_scan_lens(const uint32_t* __restrict__
     if (t == 1023) offs[n] = part[1023];
 }
 
+// the workspace slots in use
+struct SlotRange {
+    PipeSlot* a;
+    PipeSlot* b;
+    PipeSlot* begin() const { return a; }
+    PipeSlot* end() const { return b; }
+};
+inline SlotRange slots_of(HostPipe* p) { return {p->slot, p->slot + p->depth}; }
+
 void pipe_release(HostPipe* p) {
-    for (PipeSlot& s : p->slot) {
+    for (PipeSlot& s : slots_of(p)) {
         (void)hipFree(s.d_syms);
         (void)hipFree(s.d_slots);
         (void)hipFree(s.d_dense);
@@ -578,7 +598,7 @@ void pipe_free(ans_gpu* g) {
     if (!p) return;
     (void)hipDeviceSynchronize();
     pipe_release(p);
-    for (PipeSlot& s : p->slot) {
+    for (PipeSlot& s : slots_of(p)) {
         (void)hipEventDestroy(s.ev_in);
         (void)hipEventDestroy(s.ev_comp);
         (void)hipEventDestroy(s.ev_meta);
@@ -595,6 +615,22 @@ void pipe_free(ans_gpu* g) {
     g->pipe = nullptr;
 }
 
+// A stream on a hardware queue of its own, its kernels restricted to the CUs of `pattern`
+// (repeated over the mask words): a CU-masked queue is never shared.  The runtime moves
+// device-to-host bytes with blit kernels on the copy stream's queue; with GPU_MAX_HW_QUEUES = 4
+// and five streams in the process that queue was shared with the second compute stream, whose
+// decode kernels then waited for every blit (tools/host_timeline.py), and a blit spread over
+// all CUs leaves none free for a decode workgroup (which fills a CU's VGPRs and LDS).
+hipError_t own_queue_stream(hipStream_t* s, uint32_t pattern) {
+    int dev = 0, ncu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess || ncu <= 0) return e != hipSuccess ? e : hipErrorInvalidDevice;
+    std::vector<uint32_t> mask((ncu + 31) / 32, pattern);
+    if (ncu % 32) mask.back() &= (1u << (ncu % 32)) - 1u;
+    return hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data());
+}
+
 // The context's pipeline with per-slot room for `syms` symbol bytes, `slots` slot bytes,
 // `dense` dense bytes and `chunks` chunks (reallocated, after draining, when it must grow).
 int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks, HostPipe** out) {
@@ -602,10 +638,11 @@ int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks,
         auto* p = new (std::nothrow) HostPipe{};
         if (!p) return ANS_E_ALLOC;
         g->pipe = p;
-        HIP_TRY(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&p->s_comp2, hipStreamNonBlocking));
-        for (PipeSlot& s : p->slot) {
+        if (const char* e = getenv("ANS_PIPE_DEPTH")) p->depth = std::min(kPipeDepthMax, std::max(2, atoi(e)));
+        HIP_TRY(own_queue_stream(&p->s_in, ~0u));
+        HIP_TRY(own_queue_stream(&p->s_out, 0x11111111u));  // device-to-host blits on a quarter of the CUs
+        HIP_TRY(own_queue_stream(&p->s_comp2, ~0u));
+        for (PipeSlot& s : slots_of(p)) {
             HIP_TRY(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s.ev_comp, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s.ev_meta, hipEventDisableTiming));
@@ -621,7 +658,7 @@ int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks,
         dense = std::max(dense, p->cap_dense);
         chunks = std::max(chunks, p->cap_chunks);
         pipe_release(p);
-        for (PipeSlot& s : p->slot) {
+        for (PipeSlot& s : slots_of(p)) {
             HIP_TRY(hipMalloc(&s.d_syms, syms + 16));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_slots), slots + 16));
             // + 256: the fast decoders read whole aligned 128-B lines around each stream, so
@@ -637,20 +674,31 @@ int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks,
         p->cap_dense = dense;
         p->cap_chunks = chunks;
     }
-    for (PipeSlot& s : p->slot) s.used = false;
+    for (PipeSlot& s : slots_of(p)) s.used = false;
     *out = p;
     return ANS_OK;
 }
 
-// Chunks per batch: about batch_bytes (default 256 MiB) of symbols.  A batch's kernels take
+// Chunks per batch: about batch_bytes (default 128 MiB) of symbols.  A batch's kernels take
 // about one chain latency (~1 ms) whatever its size until it fills the GPU, so batches must
-// be large; 256 MiB measured best for the round trip.
-constexpr uint64_t kPipeBatchBytes = 256ull << 20;
+// be large; 128 MiB batches through six workspace slots measured best for the round trip
+// (tools/gpu_pipe_sweep.sh), with the workspace of three 256-MiB slots.
+constexpr uint64_t kPipeBatchBytes = 128ull << 20;
 uint64_t pipe_batch_chunks(const ans_gpu* g, uint64_t nchunks, uint64_t chunk_bytes) {
     const uint64_t target = g->batch_bytes ? g->batch_bytes : kPipeBatchBytes;
     uint64_t b = target / (chunk_bytes ? chunk_bytes : 1);
     if (b < 1) b = 1;
     return b < nchunks ? b : nchunks;
+}
+
+// Batch boundaries (chunk indices, first 0, last nchunks): batches of B chunks.  (Batches
+// ramping up and down in size at the ends were measured too: with enough workspace slots
+// they gained nothing over equal 128-MiB batches)
+std::vector<uint64_t> pipe_cuts(uint64_t nchunks, uint64_t B) {
+    std::vector<uint64_t> cuts{0};
+    for (uint64_t c = B; c < nchunks; c += B) cuts.push_back(c);
+    cuts.push_back(nchunks);
+    return cuts;
 }
 
 // Encode from host symbols into a host dense container.  Batch b: H2D (s_in) -> encode,
@@ -670,15 +718,16 @@ int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(p->d_status, 0, sizeof(uint32_t), gt->g->stream));
     HIP_TRY(hipStreamSynchronize(gt->g->stream));
-    const uint64_t nbatch = (nchunks + B - 1) / B;
+    const std::vector<uint64_t> cuts = pipe_cuts(nchunks, B);
+    const uint64_t nbatch = cuts.size() - 1;
     const auto* src = static_cast<const uint8_t*>(syms);
     bool copy = out != nullptr;
     int len_err = ANS_OK;
     uint64_t acc = 0;
     auto enqueue = [&](uint64_t b) -> int {
-        PipeSlot& s = p->slot[b % kPipeDepth];
+        PipeSlot& s = p->slot[b % p->depth];
         const hipStream_t sc = (b & 1) ? p->s_comp2 : gt->g->stream;
-        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
+        const uint64_t c0 = cuts[b], nc = cuts[b + 1] - c0, n0 = c0 * chunk_len;
         const uint64_t nb = std::min(n - n0, nc * chunk_len);
         if (s.used) HIP_TRY(hipStreamWaitEvent(p->s_in, s.ev_comp, 0));  // symbols of batch b - depth consumed
         HIP_TRY(hipMemcpyAsync(s.d_syms, src + n0 * w, nb * w, hipMemcpyHostToDevice, p->s_in));
@@ -702,8 +751,8 @@ int pipe_encode(ans_gpu_table* gt, const void* syms, uint64_t n, uint64_t chunk_
         return ANS_OK;
     };
     auto finish = [&](uint64_t b) -> int {
-        PipeSlot& s = p->slot[b % kPipeDepth];
-        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0);
+        PipeSlot& s = p->slot[b % p->depth];
+        const uint64_t c0 = cuts[b], nc = cuts[b + 1] - c0;
         HIP_TRY(hipEventSynchronize(s.ev_meta));
         const uint64_t bt = s.h_offs[0];
         if (copy && acc + bt > out_cap) {
@@ -749,11 +798,12 @@ int pipe_decode(ans_gpu_table* gt, const uint8_t* in, const uint64_t* offsets, c
     constexpr uint64_t w = sizeof(Sym);
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     const uint64_t B = pipe_batch_chunks(gt->g, nchunks, chunk_len * w);
-    const uint64_t nbatch = (nchunks + B - 1) / B;
+    const std::vector<uint64_t> cuts = pipe_cuts(nchunks, B);
+    const uint64_t nbatch = cuts.size() - 1;
     std::vector<uint64_t> lo(nbatch), span(nbatch);
     uint64_t max_span = 0;
     for (uint64_t b = 0; b < nbatch; ++b) {
-        const uint64_t c0 = b * B, c1 = std::min(nchunks, c0 + B);
+        const uint64_t c0 = cuts[b], c1 = cuts[b + 1];
         uint64_t l = ~0ull, h = 0;
         for (uint64_t j = c0; j < c1; ++j) {
             l = std::min(l, offsets[j]);
@@ -771,9 +821,9 @@ int pipe_decode(ans_gpu_table* gt, const uint8_t* in, const uint64_t* offsets, c
     HIP_TRY(hipStreamSynchronize(gt->g->stream));
     auto* dst = static_cast<uint8_t*>(out);
     for (uint64_t b = 0; b < nbatch; ++b) {
-        PipeSlot& s = p->slot[b % kPipeDepth];
+        PipeSlot& s = p->slot[b % p->depth];
         const hipStream_t sc = (b & 1) ? p->s_comp2 : gt->g->stream;
-        const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
+        const uint64_t c0 = cuts[b], nc = cuts[b + 1] - c0, n0 = c0 * chunk_len;
         const uint64_t nb = std::min(n - n0, nc * chunk_len);
         if (s.used) {
             HIP_TRY(hipEventSynchronize(s.ev_in));  // staging of batch b - depth uploaded
@@ -977,7 +1027,7 @@ int pipe_encode_mapped(ans_gpu_table* gt, const uint8_t* syms_dev, uint64_t n, u
     HIP_TRY(hipStreamSynchronize(s0));
     const uint64_t nbatch = (nchunks + B - 1) / B;
     for (uint64_t b = 0; b < nbatch; ++b) {
-        PipeSlot& s = p->slot[b % kPipeDepth];
+        PipeSlot& s = p->slot[b % p->depth];
         const hipStream_t sc = (b & 1) ? p->s_comp2 : s0;
         const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
         const uint64_t nb = std::min(n - n0, nc * chunk_len);
@@ -1060,7 +1110,7 @@ int pipe_decode_mapped(ans_gpu_table* gt, const uint8_t* in_dev, const uint64_t*
     HIP_TRY(hipMemsetAsync(p->d_status, 0, sizeof(uint32_t), s0));
     HIP_TRY(hipStreamSynchronize(s0));
     for (uint64_t b = 0; b < nbatch; ++b) {
-        PipeSlot& s = p->slot[b % kPipeDepth];
+        PipeSlot& s = p->slot[b % p->depth];
         const hipStream_t sc = (b & 1) ? p->s_comp2 : s0;
         const uint64_t c0 = b * B, nc = std::min(B, nchunks - c0), n0 = c0 * chunk_len;
         const uint64_t nb = std::min(n - n0, nc * chunk_len);

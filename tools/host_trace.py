@@ -21,6 +21,8 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     n, L = 1 << log2n, 4096
     g = A.Gpu(0)
+    if os.environ.get("HT_BATCH_MB"):  # pipeline batch size (ans_gpu_set_batch_bytes)
+        A._check(A.lib().ans_gpu_set_batch_bytes(g.h, int(os.environ["HT_BATCH_MB"]) << 20), "batch")
     gt = A.GpuTable(g, A.Categorical(A.c3_masses()))
     d = torch.empty(n, dtype=torch.uint8, device="cuda")
     gt.dev_gen_iid(1, 0, n, d, 1, None)
