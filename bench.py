@@ -277,16 +277,19 @@ def dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap, steps, warmu
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     for k in range(steps):
         step(events[k])
-    torch.cuda.synchronize()
-    enc = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    dec = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
-    ok = torch.equal(out, syms) and int(offs[nchunks].item()) == int(lens.to(torch.int64).sum().item())
-    return {"encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
-            "gib_s": round(n * sym_bytes / ((enc + dec) * 1e-3) / 2**30, 3),
-            "container_bytes": int(offs[nchunks].item()),
-            "what": "ans_dev_encode_dense (encode + length scan + pack) and ans_dev_decode_chunks on the "
-                    "packed container in place; round trip verified",
-            "ok": ok}
+
+    def finish():  # (after the headline: no host synchronisation between the two passes)
+        torch.cuda.synchronize()
+        enc = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+        dec = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+        ok = torch.equal(out, syms) and int(offs[nchunks].item()) == int(lens.to(torch.int64).sum().item())
+        return {"encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
+                "gib_s": round(n * sym_bytes / ((enc + dec) * 1e-3) / 2**30, 3),
+                "container_bytes": int(offs[nchunks].item()),
+                "what": "ans_dev_encode_dense (encode + length scan + pack) and ans_dev_decode_chunks on the "
+                        "packed container in place; round trip verified",
+                "ok": ok}
+    return finish
 
 
 def kernel_name(A, gt, which, sym_bytes):
@@ -480,30 +483,33 @@ def main():
         n = 1 << log2n
         start, total_n = rank * n, world * n
     L = args.chunk_len
-    # the C4 sub-object runs first: besides its own numbers it is the ~0.1 s of GPU work after
-    # which the clocks have settled (at --warmup 5 the headline otherwise charged ~2.5% of the
-    # clock ramp to the kernels: 497 vs 511 GiB/s at --warmup 30 on one box)
-    c4, c4_row = None, None
-    if args.config != "c4" and not args.no_c4:
-        c4_row, c4_names, c4_n, c4_norm = c4_pass(ctx, args)  # [elapsed, enc_ms, dec_ms, comp, bad]
-        torch.cuda.empty_cache()
     masses = getattr(A, masses_name)()
     gt, cap, nchunks, syms, slots, lens, out = workload(ctx, masses, sym_bytes, seed, start, n, L)
 
+    # The dense-container pass (the wire format: its own events, read and verified after the
+    # headline) is queued just before the headline, with no host synchronisation in between.
+    # The GPU's clocks fall back after even a short idle gap and take ~50 ms of continuous work
+    # to recover: with the dense pass read out in between, the driver's --warmup 5 left the
+    # headline 2.5% below its steady state (497 vs 511 GiB/s at --warmup 30 on one box; queued
+    # this way, 513 at either).
+    dense_finish = None if args.no_dense else dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap,
+                                                         min(args.steps, 10), args.warmup)
+
     elapsed, enc_ms, dec_ms = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out,
                                                 args.steps, args.warmup)
+    dense = None if dense_finish is None else dense_finish()
+    dense_bad = dense is not None and not dense.pop("ok")
 
     # ---- verification (outside the timed region); every rank learns whether any failed
     st = ctx.gpu.status(ctx.status, ctx.stream)
-    bad = 1.0 if (st != 0 or not torch.equal(out, syms)) else 0.0
+    bad = 1.0 if (dense_bad or st != 0 or not torch.equal(out, syms)) else 0.0
     comp_bytes = int(lens.to(torch.int64).sum().item())
-    # (its own warmup: clocks drop while the slot pass is verified; at most 10 timed steps)
-    dense = None if args.no_dense else dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap,
-                                                  min(args.steps, 10), args.warmup)
-    if dense is not None and (not dense.pop("ok") or ctx.gpu.status(ctx.status, ctx.stream) != 0):
-        bad = 1.0
     del slots, out
     torch.cuda.empty_cache()
+
+    c4, c4_row = None, None
+    if args.config != "c4" and not args.no_c4:
+        c4_row, c4_names, c4_n, c4_norm = c4_pass(ctx, args)  # [elapsed, enc_ms, dec_ms, comp, bad]
 
     # every rank's [elapsed, bad, enc_ms, dec_ms, n, comp_bytes] (+ its c4 row)
     rows = ctx.gather([elapsed, bad, enc_ms, dec_ms, float(n), float(comp_bytes)] + (c4_row or []))
