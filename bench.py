@@ -492,8 +492,9 @@ def main():
     # to recover: with the dense pass read out in between, the driver's --warmup 5 left the
     # headline 2.5% below its steady state (497 vs 511 GiB/s at --warmup 30 on one box; queued
     # this way, 513 at either).
+    # (20 warm-up steps of its own at least: ~50 ms, the clocks' settling time)
     dense_finish = None if args.no_dense else dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap,
-                                                         min(args.steps, 10), args.warmup)
+                                                         min(args.steps, 10), max(args.warmup, 20))
 
     elapsed, enc_ms, dec_ms = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out,
                                                 args.steps, args.warmup)
