@@ -834,6 +834,7 @@ struct DecChain {
             put_page(top - 1);  // top-2 stays in the low half
         }
         low = top - 1;
+        lim = 64 * low + 60;
         P = len - 4;
         read_window();
         head = 0;
@@ -847,10 +848,14 @@ struct DecChain {
             read_window();
         }
     }
+    // page low+1 is no longer read once ((P >> 2) + 1) >> 4 <= low, i.e. P < lim = 64 low + 60
+    // (floor division throughout, negative positions included): one compare per point
+    int32_t lim;
     __device__ __forceinline__ void point() {
-        if ((((P >> 2) + 1) >> 4) <= low) {  // page low+1 is no longer read: land the one below
+        if (P < lim) {  // land the page below
             put_page(low - 1);
             --low;
+            lim -= 64;
             if (!(low & 1)) fetch_pair((low >> 1) - 1);  // the next page (low-1, odd) opens a new pair
         }
     }

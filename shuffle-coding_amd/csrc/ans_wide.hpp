@@ -334,6 +334,7 @@ struct DecChainW {
             land(top - 1);                // top-2 stays in the low half
         }
         low = top - 1;
+        lim = 64 * low + 60;
         P = len - 4;
         read_window();
         head = 0;
@@ -347,10 +348,13 @@ struct DecChainW {
         }
     }
     // at a point (after s_waitcnt vmcnt(0)): land page low-1 once page low+1 is no longer read
+    // (((P >> 2) + 1) >> 4 <= low  <=>  P < lim = 64 low + 60: one compare per point)
+    int32_t lim;
     __device__ __forceinline__ void point() {
-        if ((((P >> 2) + 1) >> 4) <= low) {
+        if (P < lim) {
             land(low - 1);
             --low;
+            lim -= 64;
             if (!(low & 1)) fetch_pair((low >> 1) - 1);  // the next page (low-1, odd) opens a new pair
         }
     }
