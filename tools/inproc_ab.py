@@ -86,8 +86,10 @@ def main():
             step(i, [torch.cuda.Event(enable_timing=True) for _ in range(3)])
     torch.cuda.synchronize()
     evs = [[], []]
-    for _ in range(iters):
-        for i in range(2):
+    for it in range(iters):
+        # the order alternates: after each synchronisation the GPU idles and its clocks drop
+        # a little, which otherwise charged ~0.5-1% to whichever build ran first
+        for i in ((0, 1) if it % 2 == 0 else (1, 0)):
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             step(i, ev)
             evs[i].append(ev)
