@@ -593,8 +593,11 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             uint4 cc[GU];
 #pragma unroll
             for (int i = 0; i < GU; ++i) cc[i] = n[i];
-#pragma unroll
-            for (int u = GU - 1; u >= 0; --u) {
+            // the eight units as eight inlined calls with compile-time indices (unroll_seq, as in
+            // k_decode): a #pragma unroll was refused for the staged kmax-4 instantiations, which
+            // then indexed cc[] in scratch (144 B per lane)
+            auto unit = [&](auto ic) __attribute__((always_inline)) {
+                constexpr int u = GU - 1 - decltype(ic)::value;  // last unit first
                 flush_ready();
                 if (u == GU / 2 - 1 && g > 0) {
                     const uint4* gsrc = src + GU * (g - 1);
@@ -602,7 +605,8 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                     for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
                 }
                 process(cc[u], static_cast<uint32_t>(g * GS + u * U));
-            }
+            };
+            unroll_seq(unit, std::make_integer_sequence<int, GU>{});
         }
     }
     point();  // the last unit's completed page: the flatten's 8 bytes may reach the ring slot it holds

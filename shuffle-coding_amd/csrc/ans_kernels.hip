@@ -82,39 +82,52 @@ __device__ __forceinline__ void wave_pack(uint8_t* __restrict__ dst, const uint8
     const uint32_t bs = (16u - dsh) & 3u;         // byte shift inside the 32-B window
     const uint32_t i0 = (16u - dsh) >> 2;         // first window dword of an output block
     uint4 carry = make_uint4(0, 0, 0, 0);         // block j0 - 1 (none before the stream)
-    for (uint32_t j0 = 0; j0 < nblk; j0 += 64) {  // (wave-uniform: every lane takes part in the DPP moves)
-        const uint32_t j = j0 + lane;
-        const uint4 b = (j < nblk && 16 * j < len) ? s16[j] : make_uint4(0, 0, 0, 0);  // only blocks holding stream bytes
-        const uint4 a = make_uint4(from_lane_below(b.x, carry.x), from_lane_below(b.y, carry.y),
-                                   from_lane_below(b.z, carry.z), from_lane_below(b.w, carry.w));
-        carry = make_uint4(__builtin_amdgcn_readlane(b.x, 63), __builtin_amdgcn_readlane(b.y, 63),
-                           __builtin_amdgcn_readlane(b.z, 63), __builtin_amdgcn_readlane(b.w, 63));
-        if (j >= nblk) continue;
-        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint32_t o[4];
-        // i0 is wave-uniform: a scalar branch picks constant register indices
-        switch (i0) {
+    // passes of up to four 64-block rounds whose loads are all issued first (four 16-B loads in
+    // flight per lane: one at a time left the copy latency-bound at ~5.6 TB/s)
+    constexpr int kR = 4;
+    for (uint32_t j0 = 0; j0 < nblk; j0 += 64 * kR) {  // (wave-uniform: every lane takes part in the DPP moves)
+        uint4 bb[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const uint32_t j = j0 + 64 * r + lane;
+            bb[r] = (j < nblk && 16 * j < len) ? s16[j] : make_uint4(0, 0, 0, 0);  // only blocks holding stream bytes
+        }
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const uint32_t j = j0 + 64 * r + lane;
+            if (j0 + 64 * r >= nblk) break;  // (uniform)
+            const uint4 b = bb[r];
+            const uint4 a = make_uint4(from_lane_below(b.x, carry.x), from_lane_below(b.y, carry.y),
+                                       from_lane_below(b.z, carry.z), from_lane_below(b.w, carry.w));
+            carry = make_uint4(__builtin_amdgcn_readlane(b.x, 63), __builtin_amdgcn_readlane(b.y, 63),
+                               __builtin_amdgcn_readlane(b.z, 63), __builtin_amdgcn_readlane(b.w, 63));
+            if (j >= nblk) continue;
+            const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint32_t o[4];
+            // i0 is wave-uniform: a scalar branch picks constant register indices
+            switch (i0) {
 #define PACK_CASE(I)                                                                 \
     case I:                                                                          \
         for (int k = 0; k < 4; ++k)                                                  \
             o[k] = (I + k + 1 < 8) ? __builtin_amdgcn_alignbyte(w[(I + k + 1) & 7], w[I + k], bs) : w[I + k]; \
         break;
-            PACK_CASE(0)
-            PACK_CASE(1)
-            PACK_CASE(2)
-            PACK_CASE(3)
-            default:
-                for (int k = 0; k < 4; ++k) o[k] = w[4 + k];  // dsh = 0: block j itself
+                PACK_CASE(0)
+                PACK_CASE(1)
+                PACK_CASE(2)
+                PACK_CASE(3)
+                default:
+                    for (int k = 0; k < 4; ++k) o[k] = w[4 + k];  // dsh = 0: block j itself
 #undef PACK_CASE
-        }
-        const uint32_t lo = j == 0 ? dsh : 0u;                           // first byte of the stream here
-        const uint32_t hi = min(16u, dsh + len - 16u * j);               // one past its last
-        if (lo == 0 && hi == 16) {
-            *reinterpret_cast<uint4*>(dbase + 16ull * j) = make_uint4(o[0], o[1], o[2], o[3]);
-        } else {
+            }
+            const uint32_t lo = j == 0 ? dsh : 0u;                           // first byte of the stream here
+            const uint32_t hi = min(16u, dsh + len - 16u * j);               // one past its last
+            if (lo == 0 && hi == 16) {
+                *reinterpret_cast<uint4*>(dbase + 16ull * j) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
 #pragma unroll
-            for (uint32_t t = 0; t < 16; ++t)
-                if (t >= lo && t < hi) dbase[16ull * j + t] = static_cast<uint8_t>(o[t >> 2] >> (8 * (t & 3)));
+                for (uint32_t t = 0; t < 16; ++t)
+                    if (t >= lo && t < hi) dbase[16ull * j + t] = static_cast<uint8_t>(o[t >> 2] >> (8 * (t & 3)));
+            }
         }
     }
 }

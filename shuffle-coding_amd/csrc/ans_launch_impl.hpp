@@ -329,7 +329,11 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
         const unsigned grid = static_cast<unsigned>((nchunks + fast::kBlock - 1) / fast::kBlock);
         const bool k32 = ft.K < (1ull << 32);
         const size_t wlds = fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
-        if (sizeof(Sym) > 1 && ft.enc_wide) {
+        // (u8 symbols never take the large-alphabet kernels: not instantiated for them)
+        bool wide = false;
+        if constexpr (sizeof(Sym) > 1) wide = ft.enc_wide;
+        if (wide) {
+            if constexpr (sizeof(Sym) > 1) {
 #define ENCV2(KM, K32, PK) fast::k_encode_w<Sym, KM, K32, PK, true><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
 #define ENCV(KM, K32) if (ft.enc_pack) ENCV2(KM, K32, true); else ENCV2(KM, K32, false)
             switch (ft.kmax) {
@@ -339,6 +343,7 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
             }
 #undef ENCV
 #undef ENCV2
+            }
         } else {  // LDS rows (ans_fast.hpp k_encode, kVar)
 #define ENCL(KM, K32, R) fast::k_encode<Sym, KM, K32, false, R, true><<<grid, fast::kBlock, fast::kEncSharedBytes, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
 #define ENCL_R(KM, K32) if (ft.enc_rare) ENCL(KM, K32, true); else ENCL(KM, K32, false)
@@ -377,12 +382,16 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
         uint32_t* vlen = reinterpret_cast<uint32_t*>(static_cast<char*>(mem) + vlen_o);
         const uint64_t units = nchunks * lpad / (16 / sizeof(Sym));
         k_span_lens<Sym><<<grid_for(nchunks), kBlock, 0, s>>>(span, nchunks, vlen);
-        if (sizeof(Sym) > 1 && ft.dec_wide) {
+        bool wide = false;  // (u8 symbols never take the large-alphabet kernels: not instantiated for them)
+        if constexpr (sizeof(Sym) > 1) wide = ft.dec_wide;
+        if (wide) {
+          if constexpr (sizeof(Sym) > 1) {
             const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
             if (ft.dec_c)
                 fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
             else
                 fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+          }
         } else {  // LDS buckets (ans_fast.hpp k_decode, kVar)
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nchunks + fast::kDecBlock - 1) / fast::kDecBlock);
