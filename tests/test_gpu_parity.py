@@ -907,13 +907,19 @@ def test_random_message_fast_kernels(gpu, which):
     _roundtrip_random(gpu, masses, syms, chunk_len, dtype, 12345)
 
 
-@pytest.mark.parametrize("which", ["c3", "c4"])
+@pytest.mark.parametrize("which", ["c3", "c4", "c3_long"])
 def test_random_message_dense_container(gpu, which):
     """ans_dev_encode_dense_ex from Message::random(seed + c): the packed bytes equal the
-    oracle's, and decoding the container in place returns the symbols."""
+    oracle's, and decoding the container in place returns the symbols (c3_long: 64-KiB
+    streams, so the pack runs many passes of four 64-block rounds and carries across them)."""
     torch = pytest.importorskip("torch")
-    masses, n, sb = (A.c3_masses(), 300 * 4096, 1) if which == "c3" else (A.c4_masses(), 200 * 4096, 2)
     seed, L = 4242, 4096
+    if which == "c3":
+        masses, n, sb = A.c3_masses(), 300 * 4096, 1
+    elif which == "c4":
+        masses, n, sb = A.c4_masses(), 200 * 4096, 2
+    else:
+        masses, n, sb, L = A.c3_masses(), 40 * 65536, 1, 65536
     gt = A.GpuTable(gpu, A.Categorical(masses))
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
