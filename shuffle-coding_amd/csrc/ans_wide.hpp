@@ -276,8 +276,10 @@ struct DecChainW {
     __device__ __forceinline__ lds_u32& row(int32_t r) const {
         return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>((static_cast<uint32_t>(r) << kWideDecRowShift) + col));
     }
+    // positions count from the stream's first byte (ans_fast.hpp DecChain::fetch_pair): pairs
+    // below the top one lie inside the stream and are read with unaligned 16-B loads
     __device__ __forceinline__ void fetch_pair(int32_t m) {
-        typedef __attribute__((address_space(1))) const v4u32 gv4;
+        typedef __attribute__((address_space(1), aligned(1))) const v4u32 gv4;
         const uint4* g = m >= 0 ? reinterpret_cast<const uint4*>(src + 128ll * m) : kZeroPair;
         const gv4* gg = reinterpret_cast<const gv4*>(reinterpret_cast<uintptr_t>(g));
 #pragma unroll
@@ -312,17 +314,33 @@ struct DecChainW {
         wx = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a + kWideDecLanes * 4));
     }
     __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
-    // the top two pages land before decoding starts; the pair below them is requested
-    // s: the stream's first byte, at any alignment (a dense container).  Positions count from
-    // the 128-B line holding it (base = s - sh), so every fetch is whole aligned lines, read
-    // only from lines that hold stream bytes; the sh bytes below the stream (another chunk's)
-    // are reached only by a corrupt stream, which the final position check reports.
+    // the top pair, which may reach past the stream's end: the aligned dwords holding stream
+    // bytes, funnelled to the stream's alignment (ans_fast.hpp DecChain::fetch_top)
+    __device__ __forceinline__ void fetch_top(int32_t m, int32_t len) {
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src) + 128ll * m;
+        const gu32* d0 = reinterpret_cast<const gu32*>(a & ~uintptr_t(3));
+        const uint32_t b = static_cast<uint32_t>(a & 3u);
+        const int32_t last = static_cast<int32_t>(((reinterpret_cast<uintptr_t>(src) + len - 1) >> 2) - (a >> 2));
+        uint32_t d[33];
+#pragma unroll
+        for (int q = 0; q < 33; ++q) d[q] = q <= last ? d0[q] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            Q[k] = make_uint4(ab(d[4 * k + 1], d[4 * k], b), ab(d[4 * k + 2], d[4 * k + 1], b),
+                              ab(d[4 * k + 3], d[4 * k + 2], b), ab(d[4 * k + 4], d[4 * k + 3], b));
+    }
+    // the top two pages land before decoding starts; the pair below them is requested.
+    // s: the stream's first byte, at any alignment (a dense container); positions count from s
+    // itself (sh = 0), so the lanes of a wave land pages at nearly the same symbols in a dense
+    // container as in slots (ans_fast.hpp DecChain::start)
     __device__ __forceinline__ void start(const uint8_t* s, int32_t slen) {
-        sh = static_cast<int32_t>(reinterpret_cast<uintptr_t>(s) & 127u);
-        src = s - sh;
-        const int32_t len = slen + sh;
+        sh = 0;
+        src = s;
+        const int32_t len = slen;
         const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
-        fetch_pair(len > 0 ? top >> 1 : -1);
+        if (len > 0) fetch_top(top >> 1, len);
+        else fetch_pair(-1);
         wait_vm();
         land(top);
         if (top & 1) {
