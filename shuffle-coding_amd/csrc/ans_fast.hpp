@@ -746,26 +746,37 @@ struct DecChain {
 
     __device__ __forceinline__ uint32_t& row(int32_t r) const { return ring[r * kDecBlock]; }
     // page p (its half of Q) into ring slot p & 1
-    __device__ __forceinline__ uint32_t put_half(int32_t r0, uint4 a0, uint4 a1, uint4 a2, uint4 a3, int32_t pos) {
-        clear_below(a0, a1, a2, a3, pos, sh);
-        const uint4 a[4] = {a0, a1, a2, a3};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            row(r0 + 4 * k + 0) = a[k].x;
-            row(r0 + 4 * k + 1) = a[k].y;
-            row(r0 + 4 * k + 2) = a[k].z;
-            row(r0 + 4 * k + 3) = a[k].w;
-        }
+    // (positions count from the stream's start, so no landed page holds another stream's
+    // bytes: pages below the start are the zero page; nothing to clear)
+    // The sixteen rows go out as eight ds_write2st64_b32 from one base address (ring row r0):
+    // rows 4 KiB apart are 16 st64 units, so rows r0..r0+15 fit the 8-bit offset fields.  As C++
+    // stores the compiler formed each row's address with its own v_add (the rows lie beyond
+    // the 16-bit byte offsets) and stored them one dword at a time.
+    template <int R0>
+    __device__ __forceinline__ uint32_t put_half(uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
+        const uint32_t base = col + kDecTableBytes + R0 * kDecBlock * 4;
+        asm volatile(
+            "ds_write2st64_b32 %0, %1, %2 offset0:0 offset1:16\n\t"
+            "ds_write2st64_b32 %0, %3, %4 offset0:32 offset1:48\n\t"
+            "ds_write2st64_b32 %0, %5, %6 offset0:64 offset1:80\n\t"
+            "ds_write2st64_b32 %0, %7, %8 offset0:96 offset1:112\n\t"
+            "ds_write2st64_b32 %0, %9, %10 offset0:128 offset1:144\n\t"
+            "ds_write2st64_b32 %0, %11, %12 offset0:160 offset1:176\n\t"
+            "ds_write2st64_b32 %0, %13, %14 offset0:192 offset1:208\n\t"
+            "ds_write2st64_b32 %0, %15, %16 offset0:224 offset1:240"
+            :
+            : "v"(base), "v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+              "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w)
+            : "memory");
         return a0.x;
     }
     // two exec-masked store sets, one per parity: as one store set from selected registers the
     // compiler spent 16 v_cndmask per landing (the barrier keeps it from merging them again)
     __device__ __forceinline__ void put_page(int32_t p) {
         if (p & 1) {
-            put_half(16, Q[4], Q[5], Q[6], Q[7], 64 * p);
-            asm volatile("" ::: "memory");
+            put_half<16>(Q[4], Q[5], Q[6], Q[7]);
         } else {
-            row(32) = put_half(0, Q[0], Q[1], Q[2], Q[3], 64 * p);  // row 32 mirrors row 0
+            row(32) = put_half<0>(Q[0], Q[1], Q[2], Q[3]);  // row 32 mirrors row 0
         }
     }
     // pages are fetched as aligned 128-B pairs (2m, 2m+1): a 64-B read leaves the other half of
