@@ -288,25 +288,35 @@ struct DecChainW {
             Q[k] = make_uint4(v.x, v.y, v.z, v.w);
         }
     }
-    // page p (its half of Q) into ring slot p & 1
+    // page p (its half of Q) into ring slot p & 1: eight ds_write2st64_b32 from the lane's
+    // column (rows 2 KiB apart are 8 st64 units, rows 0..31 within the 8-bit offset fields);
+    // pages count from the stream's start, so none holds another stream's bytes
+    template <int R0>
+    __device__ __forceinline__ void land_half(uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
+        constexpr int o = 8 * R0;
+        asm volatile(
+            "ds_write2st64_b32 %0, %1, %2 offset0:%17 offset1:%18\n\t"
+            "ds_write2st64_b32 %0, %3, %4 offset0:%19 offset1:%20\n\t"
+            "ds_write2st64_b32 %0, %5, %6 offset0:%21 offset1:%22\n\t"
+            "ds_write2st64_b32 %0, %7, %8 offset0:%23 offset1:%24\n\t"
+            "ds_write2st64_b32 %0, %9, %10 offset0:%25 offset1:%26\n\t"
+            "ds_write2st64_b32 %0, %11, %12 offset0:%27 offset1:%28\n\t"
+            "ds_write2st64_b32 %0, %13, %14 offset0:%29 offset1:%30\n\t"
+            "ds_write2st64_b32 %0, %15, %16 offset0:%31 offset1:%32"
+            :
+            : "v"(col), "v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+              "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w),
+              "i"(o), "i"(o + 8), "i"(o + 16), "i"(o + 24), "i"(o + 32), "i"(o + 40), "i"(o + 48), "i"(o + 56),
+              "i"(o + 64), "i"(o + 72), "i"(o + 80), "i"(o + 88), "i"(o + 96), "i"(o + 104), "i"(o + 112), "i"(o + 120)
+            : "memory");
+    }
     __device__ __forceinline__ void land(int32_t p) {
-        const int32_t r0 = (p & 1) * 16;
-        uint4 a0, a1, a2, a3;
         if (p & 1) {
-            a0 = Q[4], a1 = Q[5], a2 = Q[6], a3 = Q[7];
+            land_half<16>(Q[4], Q[5], Q[6], Q[7]);
         } else {
-            a0 = Q[0], a1 = Q[1], a2 = Q[2], a3 = Q[3];
+            land_half<0>(Q[0], Q[1], Q[2], Q[3]);
+            row(32) = Q[0].x;  // row 32 mirrors row 0
         }
-        clear_below(a0, a1, a2, a3, 64 * p, sh);
-        const uint4 a[4] = {a0, a1, a2, a3};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            row(r0 + 4 * k + 0) = a[k].x;
-            row(r0 + 4 * k + 1) = a[k].y;
-            row(r0 + 4 * k + 2) = a[k].z;
-            row(r0 + 4 * k + 3) = a[k].w;
-        }
-        if (!(p & 1)) row(32) = a0.x;
     }
     __device__ __forceinline__ void read_window() {
         const uint32_t a = ((static_cast<uint32_t>(P) << (kWideDecRowShift - 2)) & (31u << kWideDecRowShift)) | col;  // row (P >> 2) & 31
