@@ -691,6 +691,8 @@ __device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rc
 // Stream bytes below the stream start (sh > 0: another chunk's bytes in a dense container)
 // read as zeros, the Zeros tail generator's bytes (src/ans.rs:160-170), exactly as below a
 // slot; only a corrupt stream reaches them.  S: one 64-B page at stream position pos.
+// (k_decode_g only: k_decode and k_decode_w count positions from the stream's first byte, so
+// their pages never hold another stream's bytes.)
 __device__ __forceinline__ uint32_t keep_from(uint32_t w, int32_t pos, int32_t sh) {
     const int32_t k = sh - pos;  // low bytes to clear
     return k <= 0 ? w : (k >= 4 ? 0u : w & (~0u << (8 * k)));
