@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <utility>
 
+#include "ans_renorm.hpp"
 #include "ans_table.hpp"
 
 namespace shuffle_coding {
@@ -350,14 +351,11 @@ struct PageOut {
 // kGlobalRows: the rows stay in global memory (alphabets above 256 symbols, e.g. C4's 65,536:
 // 1 MiB of rows, L2-resident); each unit's rows are then requested at the point BEFORE the
 // unit that uses them, so their latency hides behind one unit of work.
-// kRare (LDS rows only): the rows whose threshold KMAX is below 2^64 are rare (C3: one symbol of
-// probability 1e-5).  Every row then reads KMAX - 1 thresholds; those rare rows carry a negative
-// rcp and add the last threshold's test on a wave-voted branch (one 8-byte LDS read, one
-// 64-bit compare and one add fewer per symbol).
+// LDS rows: one renorm test per push whatever KMAX is (enc_thr below).
 // kVar (LDS rows only): chunk c holds vlen[c] <= chunk_len symbols at the start of its stride
 // (staged ragged / variable-length chunks, ans_kernels.hip launch_staged_encode); the pushes
 // past vlen[c], all in its first-coded group, are skipped.
-template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kRare = false, bool kVar = false>
+template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kVar = false>
 __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTable t, const Sym* __restrict__ syms,
                                                                          uint64_t chunk_len, uint64_t nfull,
                                                                          uint8_t* __restrict__ slots, uint64_t slot_cap,
@@ -380,18 +378,11 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         for (uint32_t i = threadIdx.x; i < nrows; i += kBlock) {
             const EncRow r = i < t.enc_rows ? t.enc[i] : EncRow{0.0, 0u, 0u};
             mcs[i] = make_uint2(r.mass, r.cum);
-            // renorm bound p*K (src/ans.rs:100): (head >> 8j) >= p*K  <=>  head > p*K*2^(8j) - 1,
-            // saturated at 2^64 - 1 (never exceeded) when p*K*2^(8j) >= 2^64
-            const uint64_t pK = static_cast<uint64_t>(r.mass) * t.K;
-            thrs[i] = (pK == 0 || (pK >> 56) != 0) ? ~0ull : (pK << 8) - 1;
-            const bool last_open = pK != 0 && (pK >> (64 - 8 * KMAX)) == 0;  // threshold KMAX < 2^64
-            rcps[i] = (kRare && (last_open || r.mass == 0)) ? -r.rcp : r.rcp;  // the rare-row flag
+            thrs[i] = enc_thr(static_cast<uint64_t>(r.mass) * t.K, t.L);
+            rcps[i] = r.rcp;  // 0 for zero mass: such a push always takes the voted branch
         }
     }
-    // a row in registers: the table row plus its first renorm threshold (from LDS).  The kernel
-    // tests KF thresholds on the common path, j = 1..KF: head > p*K*2^(8j) - 1 is
-    // (head >> 8(j-1)) > thr, exactly (also where p*K*2^(8j) saturates: then head >> 8(j-1) < p*K*2^8)
-    constexpr int KF = kRare ? KMAX - 1 : KMAX;
+    // a row in registers: the table row plus its renorm word (enc_thr)
     struct Row {
         EncRow e;
         uint64_t thr;
@@ -421,9 +412,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
     Funnel f{0, 0, 0, ring.col, ring.col};
     uint32_t fp = 0, over = 0;
-    uint32_t minmass = ~0u;  // 0 after a zero-mass / out-of-range symbol; accumulated by an
-                             // opaque v_min so the compiler cannot sink the test to the loop end
-                             // (it did, keeping every row alive and spilling)
+    uint32_t minmass = ~0u;  // 0 after a zero-mass / out-of-range symbol (push_one's voted branch)
 
     auto point = [&]() __attribute__((always_inline)) {
         wait_vm();
@@ -444,18 +433,15 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         if constexpr (KMAX >= 4) k += (head >> 32) >= pK ? 1u : 0u;
         return k;
     };
-    // the same as 8k: the thresholds grow with j, so the last one exceeded gives k, and the
-    // count is one v_cndmask per threshold (one LDS row read instead of KF: the encoder is
-    // co-limited by LDS bandwidth and bank conflicts, and a 64-bit shift is cheaper)
-    auto bytes_out_thr8 = [&](uint64_t thr) __attribute__((always_inline)) {
-        uint32_t k8 = 0;
-#pragma unroll
-        for (int j = 0; j < KF; ++j) k8 = (head >> (8 * j)) > thr ? 8u * (j + 1) : k8;
-        return k8;
+    // 8k from the row's renorm word w = T + 8 k0 (enc_thr): k = k0 + [head >= T], and with T's
+    // low byte zero, head >= T iff (head | 0xFF) > w
+    auto bytes_out_w8 = [&](uint64_t w) __attribute__((always_inline)) {
+        const bool up = mk64(hi32(head), lo32(head) | 0xFFu) > w;
+        return (lo32(w) & 0xFFu) + (up ? 8u : 0u);
     };
-    // kRare kernels flag zero-mass rows as rare and take their mass on the voted branch
+    // a zero-mass row (rcp 0: q_est 0, so rm = lo32(head) >= 0 = p) always takes the voted
+    // branch, which records it (the reference's assert_ne!(p, 0), src/ans.rs:98)
     auto push_one = [&](const EncRow& e, uint32_t k8) __attribute__((always_inline)) {
-        if constexpr (!kRare) asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(e.mass));  // kept in place
         f.push(lo32(head), k8);
         head >>= k8;
         // q = head / p, r = head % p (src/ans.rs:101-102), then head = norm * q + cdf(x, r)
@@ -469,6 +455,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         uint32_t rm = lo32(head) - lo32(qb) * e.mass;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= e.mass) != 0, 0)) {
             if (rm >= e.mass) {
+                minmass = min(minmass, e.mass);
                 const int64_t r = static_cast<int64_t>(head - (qb - 0x4330000000000000ull) * e.mass);
                 const int64_t d = r < 0 ? -1 : 1;
                 qb += static_cast<uint64_t>(d);
@@ -498,24 +485,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             const Row e = e_next;
             if (j > 0) e_next = row_at(roff_rt(unit, j - 1));
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
-            uint32_t k8 = bytes_out_thr8(e.thr);
-            if constexpr (kRare) {
-                EncRow r = e.e;
-                const uint32_t rh = hi32(static_cast<uint64_t>(__double_as_longlong(r.rcp)));
-                const bool rare = static_cast<int32_t>(rh) < 0;
-                uint64_t any_rare;  // a 32-bit compare of the sign word (the compiler widened it to 64)
-                asm volatile("v_cmp_gt_i32_e64 %0, 0, %1" : "=s"(any_rare) : "v"(rh));
-                if (__builtin_expect(any_rare != 0, 0)) {
-                    if (rare) {
-                        k8 = (head >> (8 * (KMAX - 1))) > e.thr ? 8u * KMAX : k8;
-                        minmass = min(minmass, r.mass);
-                        r.rcp = -r.rcp;
-                    }
-                }
-                push_one(r, k8);
-            } else {
-                push_one(e.e, k8);
-            }
+            push_one(e.e, bytes_out_w8(e.thr));
         }
     };
     auto request_rows = [&](const uint4& unit, EncRow* buf) __attribute__((always_inline)) {
@@ -581,6 +551,16 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             const uint4* gsrc = src + GU * (ngroups - 1);
 #pragma unroll
             for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
+            // a first head at or above 2^8 L (Message::random: up to 2^64 - 1) emits at least one
+            // byte in the first push whatever the symbol (p*K*2^8 <= 2^8 L); emitting it here
+            // leaves head in [L, 2^8 L), where enc_thr's one test is exact
+            const bool big = (head >> 8) >= t.L;
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(big) != 0, 0)) {
+                if (big) {
+                    f.push(lo32(head), 8);
+                    head >>= 8;
+                }
+            }
         }
         auto flush_ready = [&]() __attribute__((always_inline)) {
             if ((f.pos8 >> 9) > fp) {

@@ -284,11 +284,13 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             if ((pK << (8 * j)) < (static_cast<u128>(1) << 64)) kmax_row[s] = j;
         kmax = std::max(kmax, kmax_row[s]);
     }
-    // rows that reach kmax: rare enough (by mass) for a wave-voted slow path?
-    u128 rare_mass = 0;
+    // a symbol holding all of a power-of-two norm (L = 2^56) is the one row fast::enc_thr cannot
+    // express (its renorm test must never hold, and every head up to 2^64 - 1 is possible)
     for (uint32_t s = 0; s < nsym; ++s)
-        if (kmax_row[s] == kmax) rare_mass += cat.masses[s];
-    ft.enc_rare = kmax >= 2 && (rare_mass << 10) <= t.norm;
+        if (cat.masses[s] == t.norm && t.L == (1ull << 56)) {
+            gt->ft = ft;
+            return ANS_OK;
+        }
     ft.enc_global = nsym > 256;
     ft.dec_usable = nsym <= 256;
     // decode buckets: the finest power-of-two width whose table fits fast::kDecTableBytes in

@@ -345,15 +345,12 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
 #undef ENCV2
             }
         } else {  // LDS rows (ans_fast.hpp k_encode, kVar)
-#define ENCL(KM, K32, R) fast::k_encode<Sym, KM, K32, false, R, true><<<grid, fast::kBlock, fast::kEncSharedBytes, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
-#define ENCL_R(KM, K32) if (ft.enc_rare) ENCL(KM, K32, true); else ENCL(KM, K32, false)
+#define ENCL(KM, K32) fast::k_encode<Sym, KM, K32, false, true><<<grid, fast::kBlock, fast::kEncSharedBytes, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
             switch (ft.kmax) {
-            case 1: if (k32) ENCL(2, true, false); else ENCL(2, false, false); break;
-            case 2: if (k32) ENCL_R(2, true); else ENCL_R(2, false); break;
-            case 3: if (k32) ENCL_R(3, true); else ENCL_R(3, false); break;
-            default: if (k32) ENCL_R(4, true); else ENCL_R(4, false); break;
+            case 1: case 2: if (k32) ENCL(2, true); else ENCL(2, false); break;
+            case 3: if (k32) ENCL(3, true); else ENCL(3, false); break;
+            default: if (k32) ENCL(4, true); else ENCL(4, false); break;
             }
-#undef ENCL_R
 #undef ENCL
         }
         const hipError_t err = hipGetLastError();  // free the staging buffer on every path
@@ -461,13 +458,12 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         const size_t lds = fast::kEncSharedBytes;  // rows (LDS-row kernels) + ring
         const bool k32 = ft.K < (1ull << 32);
-#define ENC(KM, K32, G, R) fast::k_encode<Sym, KM, K32, G, R><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
-#define ENC_KMAX(G, R)                                                         \
-        switch (ft.kmax) {                                                     \
-        case 1: if (k32) ENC(2, true, G, false); else ENC(2, false, G, false); break; \
-        case 2: if (k32) ENC(2, true, G, R); else ENC(2, false, G, R); break;  \
-        case 3: if (k32) ENC(3, true, G, R); else ENC(3, false, G, R); break;  \
-        default: if (k32) ENC(4, true, G, R); else ENC(4, false, G, R); break; \
+#define ENC(KM, K32, G) fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+#define ENC_KMAX(G)                                                   \
+        switch (ft.kmax) {                                            \
+        case 1: case 2: if (k32) ENC(2, true, G); else ENC(2, false, G); break; \
+        case 3: if (k32) ENC(3, true, G); else ENC(3, false, G); break; \
+        default: if (k32) ENC(4, true, G); else ENC(4, false, G); break; \
         }
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
@@ -482,16 +478,12 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
 #undef ENCW
 #undef ENCW2
             } else if (ft.enc_global) {
-                ENC_KMAX(true, false)
-            } else if (ft.enc_rare) {
-                ENC_KMAX(false, true)
+                ENC_KMAX(true)
             } else {
-                ENC_KMAX(false, false)
+                ENC_KMAX(false)
             }
-        } else if (ft.enc_rare) {
-            ENC_KMAX(false, true)
         } else {
-            ENC_KMAX(false, false)
+            ENC_KMAX(false)
         }
 #undef ENC_KMAX
 #undef ENC

@@ -99,8 +99,6 @@ struct FastTable {
     uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
     uint32_t dec_global;  // decode fast path for nsym > 256 (k_decode_g, buckets in global memory)
     uint32_t dec_far;     // some LDS bucket holds three or more cdf boundaries (slow path needed)
-    uint32_t enc_rare;    // the rows that can emit kmax bytes carry at most 2^-10 of the mass:
-                          // the encoder's fast path tests kmax - 1 thresholds (ans_fast.hpp kRare)
     uint32_t enc_wide;    // large alphabet with norm >= 2^22: ans_wide.hpp k_encode_w (cdf rows)
     uint32_t enc_nl;      // k_encode_w: symbols below enc_nl read their cdf pair from LDS
     // k_decode_w (ans_wide.hpp): the icdf of cf < dec_w_cpre = cdf(dec_w_nlp) from LDS
