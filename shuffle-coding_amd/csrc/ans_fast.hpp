@@ -628,24 +628,31 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 // would overflow, and X >> 8 < 2^56 = L never needs one byte less).
 // kJ4 = false: no pop leaves the high word zero (kmax <= 3: p*K >= 2^32 for every symbol, and
 // a pop leaves head >= p*q >= p*K), so js = clz >> 3 needs no clamp.
+// Returns 8k.  The permute selector (7-js, 6-js, 5-js, 4-js) is the high word of the byte ramp
+// 0x0706050403020100 shifted left by 8js: one 64-bit shift of the bit count 8js = clz & ~7,
+// where the byte count took a shift, a broadcasting v_perm and a subtract.
 template <bool kJ4 = true>
-__device__ __forceinline__ uint32_t renorm_up(uint64_t& head, uint32_t W, uint64_t L, uint32_t hL8) {
+__device__ __forceinline__ uint32_t renorm_up8(uint64_t& head, uint32_t W, uint64_t L, uint32_t hL8) {
     const uint32_t h1 = hi32(head), h0 = lo32(head);
     uint32_t fb;
     asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
-    const uint32_t js = kJ4 ? min(fb >> 3, 4u) : fb >> 3;
-    const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(js, js, 0u);
+    const uint32_t m = kJ4 ? min(fb, 32u) & 0x38u : fb & 0x18u;  // 8 js
+    const uint32_t sel = hi32(0x0706050403020100ull << m);
     const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
     head = mk64(xj1, xj0);
-    uint32_t k = js;
+    uint32_t m8 = m;
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(xj1 >= hL8) != 0, 0)) {
         const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
-        if (js != 0 && mk64(xm1, xm0) >= L) {
+        if (m != 0 && mk64(xm1, xm0) >= L) {
             head = mk64(xm1, xm0);
-            k = js - 1;
+            m8 = m - 8;
         }
     }
-    return k;
+    return m8;
+}
+template <bool kJ4 = true>
+__device__ __forceinline__ uint32_t renorm_up(uint64_t& head, uint32_t W, uint64_t L, uint32_t hL8) {
+    return renorm_up8<kJ4>(head, W, L, hL8) >> 3;
 }
 __host__ __device__ inline uint32_t renorm_screen(uint64_t L) {
     const uint64_t h = (L >> 32) << 8;
@@ -718,7 +725,7 @@ struct DecChain {
     uint32_t* ring;  // &ring[0][lane]
     const uint8_t* src;
     uint4 Q[8];  // the aligned page pair (2m, 2m+1) not yet landed: one 128-B L2 line per fetch
-    int32_t low, P, sh;  // sh: the stream start within its 128-B line
+    int32_t low, P8, sh;  // P8 = 8 P (P: the window's stream position); sh = 0 (stream-relative)
     uint32_t W;
     uint64_t head;
     // per-step values between the phases
@@ -798,14 +805,19 @@ struct DecChain {
     }
     // W = bytes [P, P+4): ring rows (P>>2)&31 and the next (row 32 mirrors row 0).  With the
     // ring base in the ds offsets the row address is one v_and_or of (P << 10) and the lane's column.
+    // The position is kept in bits (P8): renorm_up8 returns bit counts, and v_alignbit_b32 takes
+    // the window's bit offset 8 (P & 3) = P8 & 31 as it is.
     uint32_t wx, wy, col;  // col = 4 * lane: the lane's byte column in the ring
     __device__ __forceinline__ void read_window() {
-        const uint32_t a = ((static_cast<uint32_t>(P) << 10) & 0x1F000u) | col;  // row (P>>2)&31
+        // row (P>>2)&31: the mask first, then one v_lshl_or (a left shift by a constant issues
+        // at the slow rate, profiles/r02_valu_microbench.txt, and v_and_or would need it)
+        uint32_t a;
+        asm("v_lshl_or_b32 %0, %1, 7, %2" : "=v"(a) : "v"(static_cast<uint32_t>(P8) & 0x3E0u), "v"(col));
         wy = lds_ld32(a + kDecTableBytes);
         wx = lds_ld32(a + kDecTableBytes + 4 * kDecBlock);
     }
-    // (v_alignbyte_b32 reads only the low two bits of its shift operand: P needs no mask)
-    __device__ __forceinline__ void form_window() { W = ab(wx, wy, static_cast<uint32_t>(P)); }
+    // (v_alignbit_b32 reads only the low five bits of its shift operand: P8 needs no mask)
+    __device__ __forceinline__ void form_window() { W = __builtin_amdgcn_alignbit(wx, wy, static_cast<uint32_t>(P8)); }
     // the top two pages land before decoding starts; the pair below them is requested.
     // s: the stream's first byte, at any alignment (a dense container).  Positions count from s
     // itself (sh = 0), so every lane's pages start at its own stream's start: streams of similar
@@ -831,8 +843,8 @@ struct DecChain {
             put_page(top - 1);  // top-2 stays in the low half
         }
         low = top - 1;
-        lim = 64 * low + 60;
-        P = len - 4;
+        lim8 = 8 * (64 * low + 60);
+        P8 = 8 * (len - 4);
         read_window();
         head = 0;
     }
@@ -841,18 +853,18 @@ struct DecChain {
         for (int g = 0; g < 9 && head < bound; ++g) {
             form_window();
             head = (head << 8) | (W >> 24);
-            P -= 1;
+            P8 -= 8;
             read_window();
         }
     }
-    // page low+1 is no longer read once ((P >> 2) + 1) >> 4 <= low, i.e. P < lim = 64 low + 60
-    // (floor division throughout, negative positions included): one compare per point
-    int32_t lim;
+    // page low+1 is no longer read once ((P >> 2) + 1) >> 4 <= low, i.e. P < 64 low + 60
+    // (floor division throughout, negative positions included): one compare per point, in bits
+    int32_t lim8;  // 8 (64 low + 60)
     __device__ __forceinline__ void point() {
-        if (P < lim) {  // land the page below
+        if (P8 < lim8) {  // land the page below
             put_page(low - 1);
             --low;
-            lim -= 64;
+            lim8 -= 512;
             if (!(low & 1)) fetch_pair((low >> 1) - 1);  // the next page (low-1, odd) opens a new pair
         }
     }
@@ -860,7 +872,7 @@ struct DecChain {
     template <bool kJ4>
     __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
         form_window();
-        P -= static_cast<int32_t>(renorm_up<kJ4>(head, W, L, hL8));
+        P8 -= static_cast<int32_t>(renorm_up8<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
         div_norm(head, norm, rcp_norm, qq, cf);
@@ -870,7 +882,7 @@ struct DecChain {
     template <bool kJ4>
     __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double magic_m1) {
         form_window();
-        P -= static_cast<int32_t>(renorm_up<kJ4>(head, W, L, hL8));
+        P8 -= static_cast<int32_t>(renorm_up8<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
         // qest_m1 with 1/norm from its SGPR pair (an asm "v" operand copied it into a VGPR pair
@@ -1033,7 +1045,8 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
     // a stream longer than its slot is foreign or corrupt: its pages would lie past the slot
-    if (!offsets && lens[c] > slot_cap) {
+    // (and no stream of a fast-path chunk reaches 2^27 bytes: positions are kept in bits)
+    if ((!offsets && lens[c] > slot_cap) || lens[c] >= (1u << 27)) {
         atomicOr(status, 1u << ANS_E_LEN);
         return;
     }
@@ -1134,7 +1147,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     }
     // assert_eq!(initial, m) with initial = the chunk's initial message (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
-    const int32_t remaining = ch.P + 4 - ch.sh;  // < 0: generated
+    const int32_t remaining = (ch.P8 >> 3) + 4 - ch.sh;  // < 0: generated
     if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
     else if (ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
 }

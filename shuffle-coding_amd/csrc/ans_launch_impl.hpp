@@ -365,7 +365,7 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
                          const uint32_t* d_lens, ChunkSpan<Sym> span, uint64_t nchunks, uint64_t lmax, int gen_kind,
                          Sym* out, uint32_t* d_status, hipStream_t s, fast::ChunkInit ini) {
     {
-        if (!staged_decode_ok<Sym>(gt) || nchunks == 0) return kNotStaged;
+        if (!staged_decode_ok<Sym>(gt) || nchunks == 0 || lmax > (1ull << 24)) return kNotStaged;
         const FastTable& ft = gt->ft;
         constexpr uint64_t GS = 128 / sizeof(Sym);
         const uint64_t lpad = std::max<uint64_t>(GS, (lmax + GS - 1) / GS * GS);
@@ -428,6 +428,9 @@ uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len, bo
     // the LDS-row encoder reads 128-B symbol groups; the decoders store 64-B symbol blocks
     const uint64_t group = (!decode && !gt->ft.enc_global) ? 128 : fast::kGroupBytes;
     if (!gt->ft.usable || (chunk_len * sizeof(Sym)) % group != 0) return 0;
+    // k_decode keeps stream positions in bits (int32): streams stay below 2^27 bytes for chunks
+    // of at most 2^24 symbols (4 bytes per push at most)
+    if (decode && chunk_len > (1ull << 24)) return 0;
     if (decode ? !gt->ft.dec_usable : (sizeof(Sym) == 1 && gt->ft.enc_global)) return 0;
     return n / chunk_len;
 }
