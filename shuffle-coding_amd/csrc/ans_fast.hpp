@@ -551,16 +551,6 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             const uint4* gsrc = src + GU * (ngroups - 1);
 #pragma unroll
             for (int i = 0; i < GU; ++i) n[i] = load_sym(gsrc + i);
-            // a first head at or above 2^8 L (Message::random: up to 2^64 - 1) emits at least one
-            // byte in the first push whatever the symbol (p*K*2^8 <= 2^8 L); emitting it here
-            // leaves head in [L, 2^8 L), where enc_thr's one test is exact
-            const bool big = (head >> 8) >= t.L;
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(big) != 0, 0)) {
-                if (big) {
-                    f.push(lo32(head), 8);
-                    head >>= 8;
-                }
-            }
         }
         auto flush_ready = [&]() __attribute__((always_inline)) {
             if ((f.pos8 >> 9) > fp) {

@@ -8,15 +8,15 @@ namespace shuffle_coding {
 namespace fast {
 
 // The LDS-row encoder's renorm word for a row with bound pK = p*K (src/ans.rs:100, 246-253):
-// a push emits k = #{j >= 1 : head >= pK * 2^8j} bytes.  Every push but a chain's first starts
-// from head in [L, 2^8 L) (L = norm*K: a push leaves head = norm*q + cdf < norm*2^8 K), and a
+// a push emits k = #{j >= 1 : head >= pK * 2^8j} bytes.  Every push starts from head in
+// [L, 2^8 L) (L = norm*K > 2^56 - norm: a push leaves head = norm*q + cdf < norm*2^8 K, and a
+// chain's initial head, Message::zeros / empty / random, lies in [2^56, 2^57)), and a
 // factor-2^8 interval holds at most one of the bounds pK*2^8j strictly inside it, so
 // k = k0 + [head >= T] with k0 = #{j : pK*2^8j <= L} and T = pK*2^8(k0+1): ONE compare.  T's low
 // byte is zero, so the word carries 8 k0 there: w = T + 8 k0.  Where T >= 2^8 L the test never
 // holds and the row uses (k0 - 1, T / 2^8 <= L: always holds) instead; for k0 = 0 that is p = norm,
 // T = 2^8 L, and with L < 2^56 no head reaches T (L = 2^56 with a mass equal to norm leaves the
 // table off the fast path: ans_kernels.hip build_fast_table).  Zero mass: never, k0 = 0.
-// (A chain's first head may lie above 2^8 L: Message::random; k_encode pre-emits its byte.)
 constexpr uint64_t enc_thr(uint64_t pK, uint64_t L) {
     if (pK == 0) return ~0xFFull;
     uint32_t k0 = 0;

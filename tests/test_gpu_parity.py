@@ -668,10 +668,11 @@ def test_boundary_tables_bit_exact(gpu, name):
 
 
 def test_rare_rows_whole_waves(gpu):
-    """The encoder's rare-row path (ans_fast.hpp kRare: rows that can emit kmax bytes hold at most
-    2^-10 of the mass, so they are tested on a wave-voted branch) under data made of them: chunks
-    of only rare symbols (every lane of a wave on the slow path), half rare, and one rare symbol
-    in an otherwise common chunk.  (CPU-checkable precondition: the table does select kRare.)"""
+    """Rows that can emit kmax = 4 bytes per push (tiny masses: the one-compare renorm word
+    ans_renorm.hpp enc_thr with k0 = 3; until r03e a wave-voted rare-row branch) under data made
+    of them: chunks of only such symbols, half of them, and one in an otherwise common chunk.
+    (CPU-checkable precondition: the table has kmax 4 and those rows hold at most 2^-10 of the
+    mass, so common data rarely reaches them.)"""
     masses = _tables_at_the_boundaries()["kmax_4"]
     norm, K = int(masses.sum()), (1 << 56) // int(masses.sum())
     kmax_row = [max([j for j in range(1, 5) if (int(m) * K) << (8 * j) < 1 << 64], default=0) for m in masses]

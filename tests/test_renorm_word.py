@@ -4,16 +4,15 @@ DESIGN.md §3.1) against the reference's renorm loop, on the CPU.
 The reference pushes a symbol of mass p after `renorm(p * K)` (src/ans.rs:100), whose
 renorm_down emits head's low byte while `head >> 8 >= p * K` (src/ans.rs:246-253).  The kernel
 computes the same count k from one 64-bit compare of (head | 0xFF) with the row's word
-w = T + 8 k0 for every head in [L, 2^8 L), and first emits one byte of a chain's first head when
-it lies at or above 2^8 L (Message::random).  This test compiles a brute-force checker with g++
-against the product header and compares both rules with the reference loop over random tables
-(norms 2^16..2^31, masses from 1 to norm) and heads drawn uniformly, next to the interval ends
-and within a few units of every bound p*K*2^8j.
+w = T + 8 k0, exact for every head in [L, 2^8 L): the heads a push leaves, and the initial heads
+of Message::zeros / empty (2^56) and Message::random ([2^56, 2^57), src/ans.rs:285-299).  This
+test compiles a brute-force checker with g++ against the product header and compares the rule
+with the reference loop over random tables (norms 2^16..2^31, masses from 1 to norm) and heads
+drawn uniformly, next to the interval ends, within a few units of every bound p*K*2^8j, and
+from the initial-head range.
 """
 import os
 import subprocess
-
-import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "shuffle-coding_amd", "csrc")
@@ -55,7 +54,7 @@ int main(int argc, char** argv) {
         if (p > norm) p = norm;
         if (p == norm && L == (1ull << 56)) { ++skipped; continue; }  // kept off the fast path
         const uint64_t pK = p * K, w = enc_thr(pK, L);
-        const u128 top = (u128)L << 8;  // heads of every push but a chain's first: [L, 2^8 L)
+        const u128 top = (u128)L << 8;  // the heads of every push: [L, 2^8 L)
         for (int h = 0; h < 48; ++h) {
             uint64_t head;
             switch (h % 4) {
@@ -80,18 +79,13 @@ int main(int argc, char** argv) {
                 ++bad;
             }
         }
-        // a chain's first head from Message::random: [2^56, 2^64); at or above 2^8 L the kernel
-        // emits one byte first, then applies the word to head >> 8
+        // initial heads: Message::zeros / empty (2^56) and Message::random, [2^56, 2^57)
         for (int h = 0; h < 8; ++h) {
-            uint64_t head = (h & 1) ? ~0ull - R() % 1000 : (1ull << 56) | (R() >> 8);
-            if (h == 2 && top < ((u128)1 << 64)) head = (uint64_t)top + R() % 256;
-            uint32_t k = 0;
-            uint64_t x = head;
-            if ((x >> 8) >= L) { x >>= 8; k = 1; }
-            k += kernel_k(x, w);
+            const uint64_t head = h == 0 ? (1ull << 56) : (1ull << 56) | (R() >> 8);
+            if (head < L || (u128)head >= top) { ++bad; printf("initial head outside [L, 2^8 L)\n"); }
             ++n;
-            if (k != ref_k(head, pK)) {
-                if (bad < 5) printf("bad first head norm=%llu p=%llu head=%llx\n", (unsigned long long)norm, (unsigned long long)p, (unsigned long long)head);
+            if (kernel_k(head, w) != ref_k(head, pK)) {
+                if (bad < 5) printf("bad initial head norm=%llu p=%llu head=%llx\n", (unsigned long long)norm, (unsigned long long)p, (unsigned long long)head);
                 ++bad;
             }
         }
