@@ -669,7 +669,7 @@ def test_boundary_tables_bit_exact(gpu, name):
 
 def test_rare_rows_whole_waves(gpu):
     """Rows that can emit kmax = 4 bytes per push (tiny masses: the one-compare renorm word
-    ans_renorm.hpp enc_thr with k0 = 3; until r03e a wave-voted rare-row branch) under data made
+    ans_renorm.hpp enc_thr with k0 = 3; until r03f a wave-voted rare-row branch) under data made
     of them: chunks of only such symbols, half of them, and one in an otherwise common chunk.
     (CPU-checkable precondition: the table has kmax 4 and those rows hold at most 2^-10 of the
     mass, so common data rarely reaches them.)"""
