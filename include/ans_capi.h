@@ -183,7 +183,9 @@ int ans_dev_encode_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, 
                           uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status, void *stream);
 /* d_offsets == NULL: chunk j's stream starts at d_in + j*slot_cap (the encoder's layout);
  * otherwise at d_in + d_offsets[j] (e.g. a dense container, at any alignment: the fast decoders
- * read it in place).  Every byte of the aligned 128-B lines holding a stream may be read. */
+ * read it in place).  Every byte of the aligned 128-B lines holding a stream may be read.
+ * A d_lens entry above slot_cap (slot layout) or of 2^27 bytes or more (no stream of a chunk
+ * the fast decoders take reaches that) is foreign or corrupt: ANS_E_LEN. */
 int ans_dev_decode_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
                           const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void *d_syms,
                           int sym_bytes, uint32_t *d_status, void *stream);
