@@ -98,13 +98,15 @@ def lib_hash(A):
     return h.hexdigest()[:16]
 
 
-def pmc_record(A, kernel_key, config, log2n, chunk_len):
+def pmc_record(A, kernel_key, config, log2n, chunk_len, pattern="*pmc*.json"):
     """The rocprofv3 PMC record of `kernel_key` on the same workload from a committed summary
-    (profiles/*pmc*.json, written by tools/pmc_summary.py --json), preferring one taken on this
-    exact library build, then the latest round; (record, source file) or (None, None)."""
+    (profiles/*pmc*.json, written by tools/pmc_summary.py --json; or, with pattern "*kstats*.json",
+    the kernel-trace --stats averages written by tools/kstats_json.py), preferring one taken on
+    this exact library build, then the latest round; (record, source file, same build) or
+    (None, None, False)."""
     best = None
     mine = lib_hash(A)
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -116,7 +118,7 @@ def pmc_record(A, kernel_key, config, log2n, chunk_len):
         rank = (d.get("lib_hash") == mine, path)
         if best is None or rank > best[0]:
             best = (rank, k, os.path.relpath(path, ROOT))
-    return (None, None) if best is None else (best[1], best[2])
+    return (None, None, False) if best is None else (best[1], best[2], best[0][0])
 
 
 def l2_ceiling():
@@ -195,6 +197,19 @@ class Ctx:
         if self.world > 1:
             self.dist.barrier()
 
+    def agree(self, err, what):
+        """Every rank reaches this collective once per phase, whether its phase succeeded or not
+        (err: this rank's exception or None); if any rank failed, every rank leaves together
+        with an error instead of the healthy ranks waiting in the next barrier for one that has
+        gone (torchrun would only reap them at its own timeout)."""
+        flags = self.gather([0.0 if err is None else 1.0])
+        bad = [r for r, f in enumerate(flags) if f[0] > 0]
+        if bad:
+            mine = f": {type(err).__name__}: {err}" if err is not None else ""
+            if self.world > 1:
+                self.dist.destroy_process_group()
+            raise SystemExit(f"rank {self.rank}: {what} failed on rank(s) {bad}{mine}")
+
     def gather(self, values):
         """Every rank's float values, as a list of lists (rank order)."""
         t = self.torch.tensor(values, dtype=self.torch.float64,
@@ -220,9 +235,11 @@ def workload(ctx, masses, sym_bytes, seed, start, n, L):
     return gt, cap, nchunks, syms, slots, lens, out
 
 
-def timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out, steps, warmup):
+def timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out, steps, warmup, pre=None):
     """warmup untimed steps, then `steps` steps bracketed by barrier + synchronize on both
-    sides; (wall seconds, mean encode ms, mean decode ms) with HIP events on ctx.stream."""
+    sides; (wall seconds, mean encode ms, mean decode ms, pre()'s result) with HIP events on
+    ctx.stream.  pre: work queued just before the warm-up (the dense pass), inside the same
+    failure agreement."""
     torch, stream, status = ctx.torch, ctx.stream, ctx.status
 
     def step(ev=None):
@@ -235,21 +252,36 @@ def timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out, ste
         if ev is not None:
             ev[2].record(stream)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
+    # a launch that raises on one rank must not leave the others in a barrier: every rank runs
+    # both barriers of the timed region whatever happens, then all agree on the outcome
+    err, pre_out = None, None
+    try:
+        if pre is not None:
+            pre_out = pre()
+        if os.environ.get("BENCH_FAIL_RANK") == str(ctx.rank):  # test knob: one rank's launch fails
+            raise RuntimeError("BENCH_FAIL_RANK")
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 (reported to every rank by ctx.agree)
+        err = e
+    ctx.agree(err, "warm-up")
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        step(events[k])
-    torch.cuda.synchronize()
+    try:
+        for k in range(steps):
+            step(events[k])
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001
+        err = e
     ctx.barrier()
     elapsed = time.perf_counter() - t0
+    ctx.agree(err, "timed steps")
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
-    return elapsed, enc_ms, dec_ms
+    return elapsed, enc_ms, dec_ms, pre_out
 
 
 def dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap, steps, warmup):
@@ -308,13 +340,22 @@ def c4_pass(ctx, args):
     n = 1 << args.c4_log2n
     L = args.chunk_len
     masses = A.c4_masses()
-    gt, cap, nchunks, syms, slots, lens, out = workload(ctx, masses, sym_bytes, seed, ctx.rank * n, n, L)
-    elapsed, enc_ms, dec_ms = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out,
-                                                args.steps, min(args.warmup, 5))
-    st = ctx.gpu.status(ctx.status, ctx.stream)
-    bad = 1.0 if (st != 0 or not torch.equal(out, syms)) else 0.0
-    comp = float(lens.to(torch.int64).sum().item())
-    names = (kernel_name(A, gt, "encode", sym_bytes), kernel_name(A, gt, "decode", sym_bytes))
+    err = None
+    try:
+        gt, cap, nchunks, syms, slots, lens, out = workload(ctx, masses, sym_bytes, seed, ctx.rank * n, n, L)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    ctx.agree(err, "c4 setup")
+    elapsed, enc_ms, dec_ms, _ = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out,
+                                                   args.steps, min(args.warmup, 5))
+    comp = 0.0
+    try:
+        st = ctx.gpu.status(ctx.status, ctx.stream)
+        bad = 1.0 if (st != 0 or not torch.equal(out, syms)) else 0.0
+        comp = float(lens.to(torch.int64).sum().item())
+    except Exception:  # noqa: BLE001 (reported in the caller's gather)
+        bad = 1.0
+    names =(kernel_name(A, gt, "encode", sym_bytes), kernel_name(A, gt, "decode", sym_bytes))
     del syms, slots, lens, out
     torch.cuda.empty_cache()
     return [elapsed, enc_ms, dec_ms, comp, bad], names, n, int(masses.sum())
@@ -484,7 +525,12 @@ def main():
         start, total_n = rank * n, world * n
     L = args.chunk_len
     masses = getattr(A, masses_name)()
-    gt, cap, nchunks, syms, slots, lens, out = workload(ctx, masses, sym_bytes, seed, start, n, L)
+    err = None
+    try:
+        gt, cap, nchunks, syms, slots, lens, out = workload(ctx, masses, sym_bytes, seed, start, n, L)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    ctx.agree(err, "setup")
 
     # The dense-container pass (the wire format: its own events, read and verified after the
     # headline) is queued just before the headline, with no host synchronisation in between.
@@ -493,18 +539,22 @@ def main():
     # headline 2.5% below its steady state (497 vs 511 GiB/s at --warmup 30 on one box; queued
     # this way, 513 at either).
     # (20 warm-up steps of its own at least: ~50 ms, the clocks' settling time)
-    dense_finish = None if args.no_dense else dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap,
-                                                         min(args.steps, 10), max(args.warmup, 20))
-
-    elapsed, enc_ms, dec_ms = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out,
-                                                args.steps, args.warmup)
+    pre = None if args.no_dense else (lambda: dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap,
+                                                         min(args.steps, 10), max(args.warmup, 20)))
+    elapsed, enc_ms, dec_ms, dense_finish = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens,
+                                                              out, args.steps, args.warmup, pre=pre)
     dense = None if dense_finish is None else dense_finish()
     dense_bad = dense is not None and not dense.pop("ok")
 
-    # ---- verification (outside the timed region); every rank learns whether any failed
-    st = ctx.gpu.status(ctx.status, ctx.stream)
-    bad = 1.0 if (dense_bad or st != 0 or not torch.equal(out, syms)) else 0.0
-    comp_bytes = int(lens.to(torch.int64).sum().item())
+    # ---- verification (outside the timed region); every rank learns whether any failed (a rank
+    # whose check itself raises reports a failure in the same gather instead of leaving it)
+    st, comp_bytes = 0, 0
+    try:
+        st = ctx.gpu.status(ctx.status, ctx.stream)
+        bad = 1.0 if (dense_bad or st != 0 or not torch.equal(out, syms)) else 0.0
+        comp_bytes = int(lens.to(torch.int64).sum().item())
+    except Exception:  # noqa: BLE001
+        bad = 1.0
     del slots, out
     torch.cuda.empty_cache()
 
@@ -541,7 +591,7 @@ def main():
     strong_split = args.strong and world > 1
 
     def valu_of(kernel, ms):
-        rec, src = (None, None) if strong_split else pmc_record(A, kernel, args.config, log2n, L)
+        rec, src, same = (None, None, False) if strong_split else pmc_record(A, kernel, args.config, log2n, L)
         if rec is None or "valu_per_wave" not in rec.get("derived", {}):
             return rec, src, None
         # one wave = 64 lanes = 64 chunks, one VALU wave-instruction per lane-step;
@@ -553,6 +603,7 @@ def main():
         clk = d.get("clock_ghz")
         return rec, src, {
             "kernel": kernel,
+            "pmc_same_build": same,  # False: the counts are another build's (the latest committed record)
             "instr_per_symbol": round(d["valu_per_wave"] / L, 2),
             "frac_at_2.4GHz": round(wave_instr * 4 / (cus * 4 * 2.4e9 * ms * 1e-3), 4),
             "clock_ghz_pmc": None if clk is None else round(clk, 3),
@@ -562,6 +613,16 @@ def main():
     rec, rec_src, valu = valu_of(dom_kernel, dom_ms)
     _, _, valu_other = valu_of(other_kernel, enc_ms if other_name == "encode" else dec_ms)
     traffic = None if rec is None else rec.get("hbm_bytes_per_launch")
+    pmc_same = bool(valu and valu["pmc_same_build"])
+    # the same fraction from the committed rocprofv3 --kernel-trace --stats average of the
+    # dominant kernel (profiles/*kstats*.json), beside the HIP-event one
+    ks, ks_src, ks_same = (None, None, False) if strong_split else pmc_record(A, dom_kernel, args.config, log2n, L,
+                                                                               pattern="*kstats*.json")
+    ks_ns = None if ks is None else ks.get("avg_ns")
+    hbm_frac = achieved / HBM_PEAK_GBS
+    # what binds: the VALU issue fraction (PMC instruction count at 4 cycles per wave64
+    # instruction) when it exceeds the HBM fraction, as it does for the integer coding kernels
+    bound = "valu-issue" if (valu and valu["frac_at_2.4GHz"] > hbm_frac) else "hbm"
 
     if rank == 0:
         per_frac = [(r[4] * sym_bytes + r[5]) / (max(r[2], r[3]) * 1e-3) / 1e9 / HBM_PEAK_GBS for r in rows]
@@ -583,6 +644,8 @@ def main():
                             f"{'in total' if args.strong else 'per GPU'}, "
                             f"{len(masses)}-symbol Categorical (norm {int(masses.sum())}), chunk_len {L}",
                 "symbols_per_gpu": n,
+                "symbols_per_rank": [int(r[4]) for r in rows],
+                "symbols_total": total_n,
                 "symbol_bytes": sym_bytes,
                 "chunk_len": L,
                 "chunks_per_gpu": nchunks,
@@ -600,16 +663,26 @@ def main():
             "host": host,
             "parity": "round trip verified on device; byte parity vs the oracle: tests/test_gpu_parity.py",
             "roofline": {
-                "bound": "hbm",
+                "bound": bound,
                 "kernel": dom_kernel,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac": round(hbm_frac, 4),
+                "frac_rocprof": None if not ks_ns else round(alg_bytes / ks_ns / HBM_PEAK_GBS, 4),
+                "rocprof_avg_ns": ks_ns,
+                "rocprof_src": ks_src,
+                "rocprof_same_build": ks_same,
                 "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),  # vs 6.29 TB/s float4 copy
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_over_alg": None if traffic is None else round(traffic / alg_bytes, 3),
                 "traffic_src": rec_src,
+                "pmc_same_build": pmc_same,
+                # 0.70 of 8 TB/s at this workload's bytes per symbol, against the chip's VALU issue
+                # rate (256 CU x 4 SIMD x 16 lanes x 2.4 GHz): the most VALU per symbol, encode and
+                # decode each, that the north_star target allows
+                "valu_per_symbol_budget_at_0.70": round(
+                    256 * 4 * 16 * 2.4e9 / (0.70 * HBM_PEAK_GBS * 1e9 / (alg_bytes / n)), 1),
                 "valu": valu,
                 "valu_other": valu_other,
                 "per_rank_frac": {"min": round(min(per_frac), 4), "max": round(max(per_frac), 4)},

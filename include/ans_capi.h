@@ -124,9 +124,12 @@ void ans_gpu_free(ans_gpu *g);
  * then run asynchronously and overlap; pageable buffers go through the runtime's staging. */
 int ans_host_alloc(size_t bytes, void **out);
 void ans_host_free(void *p);
-/* Symbol bytes per batch of the host-buffer pipeline below (0 = the default, 256 MiB).
+/* Symbol bytes per batch of the host-buffer pipeline below (0 = the default, 128 MiB).
  * Batches overlap their H2D copy, kernels and D2H copy on separate streams. */
 int ans_gpu_set_batch_bytes(ans_gpu *g, uint64_t batch_bytes);
+/* The pipeline's workspace slots: 0 until the first host-buffer call builds the pipeline, then
+ * ANS_PIPE_DEPTH as read at that moment (2..8; default 6). */
+int ans_gpu_pipe_depth(const ans_gpu *g, int *depth);
 /* uploads the table (and its derived reciprocal / icdf-bucket data) to the device */
 int ans_gpu_table_create(ans_gpu *g, const ans_table *t, ans_gpu_table **out);
 void ans_gpu_table_free(ans_gpu_table *gt);
@@ -140,7 +143,9 @@ void ans_gpu_table_free(ans_gpu_table *gt);
 #define ANS_PATH_DEC_WIDE 32u   /* large alphabet: LDS prefix icdf + global buckets */
 #define ANS_PATH_DEC_COMPACT 64u /* ... whose global buckets are 16 B (u16 candidate offsets) */
 #define ANS_PATH_ENC_PACKED 128u /* large-alphabet encoder with the packed (u32 base + u16) LDS prefix */
-#define ANS_PATH_DEC_U 256u     /* LDS decoder without the quotient fix-up (u-domain tables; u8 symbols) */
+#define ANS_PATH_DEC_U 256u     /* LDS decoder without the quotient fix-up (u-domain tables): applies to
+                                  * sym_bytes == 1 only; u16 / u32 decodes of the same table run the
+                                  * row decoder (kModeRows: the same bytes, one fix-up more) */
 int ans_gpu_table_paths(const ans_gpu_table *gt, uint32_t *paths);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);
@@ -183,7 +188,9 @@ int ans_dev_encode_chunks(ans_gpu_table *gt, const void *d_syms, int sym_bytes, 
                           uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status, void *stream);
 /* d_offsets == NULL: chunk j's stream starts at d_in + j*slot_cap (the encoder's layout);
  * otherwise at d_in + d_offsets[j] (e.g. a dense container, at any alignment: the fast decoders
- * read it in place).  Every byte of the aligned 128-B lines holding a stream may be read.
+ * read it in place).  The fast decoders (k_decode, k_decode_w) read no byte outside the
+ * stream; k_decode_g (norm < 2^22 with more than 256 symbols) may read every byte of the
+ * aligned 128-B lines holding a stream, so such a container needs 128 readable bytes past its end.
  * A d_lens entry above slot_cap (slot layout) or of 2^27 bytes or more (no stream of a chunk
  * the fast decoders take reaches that) is foreign or corrupt: ANS_E_LEN. */
 int ans_dev_decode_chunks(ans_gpu_table *gt, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,

@@ -74,6 +74,7 @@ SIGNATURES = {
     "ans_gpu_create": (ci, [ci, ctypes.POINTER(vp)]),
     "ans_gpu_free": (None, [vp]),
     "ans_gpu_set_batch_bytes": (ci, [vp, u64]),
+    "ans_gpu_pipe_depth": (ci, [vp, ctypes.POINTER(ci)]),
     "ans_host_alloc": (ci, [sz, ctypes.POINTER(vp)]),
     "ans_host_free": (None, [vp]),
     "ans_gpu_table_create": (ci, [vp, vp, ctypes.POINTER(vp)]),
@@ -572,8 +573,14 @@ class Gpu:
             self.h = None
 
     def set_batch_bytes(self, batch_bytes):
-        """Symbol bytes per batch of the host-buffer pipeline (0 = default, 256 MiB)."""
+        """Symbol bytes per batch of the host-buffer pipeline (0 = default, 128 MiB)."""
         _check(lib().ans_gpu_set_batch_bytes(self.h, batch_bytes), "ans_gpu_set_batch_bytes")
+
+    def pipe_depth(self):
+        """Workspace slots of the host-buffer pipeline (0 before its first call)."""
+        d = ci(0)
+        _check(lib().ans_gpu_pipe_depth(self.h, ctypes.byref(d)), "ans_gpu_pipe_depth")
+        return d.value
 
     def status(self, d_status, stream=None):
         st = ci(0)

@@ -676,8 +676,9 @@ int pipe_get(ans_gpu* g, size_t syms, size_t slots, size_t dense, size_t chunks,
         for (PipeSlot& s : slots_of(p)) {
             HIP_TRY(hipMalloc(&s.d_syms, syms + 16));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_slots), slots + 16));
-            // + 256: the fast decoders read whole aligned 128-B lines around each stream, so
-            // the last stream of a batch may touch the line past its span
+            // + 256: k_decode_g (the non-wide large-alphabet decoder, norm < 2^22) reads whole
+            // aligned 128-B lines around each stream, so the last stream of a batch may touch the
+            // line past its span (k_decode and k_decode_w read only the stream's own bytes)
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dense), dense + 256));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_lens), sizeof(uint32_t) * chunks + 16));
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_offs), sizeof(uint64_t) * (chunks + 1) + 16));
@@ -1257,6 +1258,12 @@ void ans_host_free(void* p) {
 int ans_gpu_set_batch_bytes(ans_gpu* g, uint64_t batch_bytes) {
     if (!g) return ANS_E_ARG;
     g->batch_bytes = batch_bytes;
+    return ANS_OK;
+}
+
+int ans_gpu_pipe_depth(const ans_gpu* g, int* depth) {
+    if (!g || !depth) return ANS_E_ARG;
+    *depth = g->pipe ? g->pipe->depth : 0;
     return ANS_OK;
 }
 

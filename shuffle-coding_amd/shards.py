@@ -182,13 +182,13 @@ def _all_gather_varlen(local, counts, starts, out, group):
         out[starts[r]:starts[r] + counts[r]] = p.cpu().numpy()[:counts[r]].view(np.uint64)
 
 
-def _dtype_of_num(num):
-    """The numpy dtype whose .num is `num` (the integer and float types a decoder returns)."""
-    for t in (np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16, np.int32, np.int64, np.bool_,
-              np.float32, np.float64):
-        if np.dtype(t).num == num:
-            return np.dtype(t)
-    raise ValueError(f"unexpected decoder dtype number {num}")
+def _dtype_of(kind, itemsize):
+    """The numpy dtype of kind character code `kind` (ord of 'u', 'i', 'b' or 'f') and `itemsize`
+    bytes: alias types (np.ulonglong, np.intc, ...) gather as their canonical dtype."""
+    k = chr(kind)
+    if k not in "uibf":
+        raise ValueError(f"unexpected decoder dtype kind {k!r}")
+    return np.dtype(bool) if k == "b" else np.dtype(f"{k}{itemsize}")
 
 
 def decode_distributed(decode_shard, data, offsets, lens, n, chunk_len, group=None, dst=0, out=None,
@@ -200,7 +200,10 @@ def decode_distributed(decode_shard, data, offsets, lens, n, chunk_len, group=No
     out=None: rank `dst` returns the n symbols, the others None.  out=path: the symbols are
     written there (`dtype` elements), each rank its own range; every rank returns None.
     dtype=None: the decoders' own dtype (the widest over the ranks that decoded symbols, agreed
-    through one all_gather); a dtype that cannot hold every decoded value raises.
+    through one all_gather, as kind and width so alias types agree); a dtype that cannot hold
+    every decoded value raises, and so do decoders mixing signed and unsigned 64-bit types.
+    (Round 3 changed the default from np.uint8 to None: files written with out=path now hold
+    the decoders' element width, e.g. 4 bytes for u32 symbols; pass dtype=np.uint8 for the old one.)
     """
     import torch.distributed as dist
 
@@ -217,9 +220,12 @@ def decode_distributed(decode_shard, data, offsets, lens, n, chunk_len, group=No
         src = np.asarray(data[base:end])
     res = np.asarray(decode_shard(np.asarray(src), off - np.uint64(base), ln, s1 - s0, chunk_len))
     if dtype is None:  # every rank must write the same element width: agree on the decoders' dtype
-        nums = _all_gather_ints([s1 - s0, res.dtype.num], group)
-        found = [_dtype_of_num(int(k)) for m, k in nums if m > 0]
+        info = _all_gather_ints([s1 - s0, ord(res.dtype.kind), res.dtype.itemsize], group)
+        found = [_dtype_of(int(k), int(w)) for m, k, w in info if m > 0]
         dtype = np.result_type(*found) if found else res.dtype
+        if found and all(f.kind in "uib" for f in found) and dtype.kind == "f":
+            # np.result_type(int64, uint64) is float64: no integer type holds both
+            raise ValueError(f"decoders disagree on signedness at 64 bits ({sorted(set(map(str, found)))})")
     dtype = np.dtype(dtype)
     local = np.ascontiguousarray(res.astype(dtype, copy=False))
     if res.size and not np.array_equal(local, res):

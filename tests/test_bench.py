@@ -39,3 +39,41 @@ def test_bench_launches_two_ranks_itself():
     assert d["per_rank_ms_per_step"]["max"] == d["ms_per_step"]
     assert d["c4"]["per_rank"]["ms_per_step"]["max"] == d["c4"]["ms_per_step"]
     assert d["c4"]["workload"].startswith("C4: 2^22 iid u16 symbols per GPU")
+    assert d["config"]["symbols_per_rank"] == [1 << 24, 1 << 24]
+
+
+def _two_ranks(extra, timeout=110, **env_extra):
+    env = dict(os.environ, BENCH_SHARE_DEVICE="1", BENCH_BACKEND="gloo", **env_extra)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", BENCH, "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+           "--no-dense", "--no-host"] + extra
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.gpu
+def test_bench_strong_scaling_two_ranks():
+    """--strong --gpus 2: the config's 2^log2n symbols in total, split into whole-chunk ranges over
+    the ranks (shards.shard_symbols); the two shards' symbol counts sum to 2^log2n and the value
+    is the whole array over the slowest rank's step."""
+    r = _two_ranks(["--strong", "--log2n", "25", "--no-c4"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    per = d["config"]["symbols_per_rank"]
+    assert len(per) == 2 and sum(per) == 1 << 25 and all(p % 4096 == 0 for p in per)
+    assert d["config"]["symbols_total"] == 1 << 25
+    assert abs(d["value"] - (1 << 25) / (d["ms_per_step"] * 1e-3) / 2**30) < 0.01 * d["value"]
+
+
+@pytest.mark.gpu
+def test_bench_failing_rank_ends_every_rank():
+    """A rank whose launch raises (test knob BENCH_FAIL_RANK) must not leave the other rank in
+    the timed region's barrier: both reach the same failure agreement and exit non-zero, well
+    inside the launcher's own timeouts."""
+    r = _two_ranks(["--log2n", "22", "--no-c4"], timeout=100, BENCH_FAIL_RANK="1")
+    assert r.returncode != 0
+    assert "failed on rank(s) [1]" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
