@@ -279,9 +279,13 @@ int ans_dev_check_renorm(ans_gpu *g, const uint64_t *d_heads, const uint32_t *d_
 int ans_dev_status(ans_gpu *g, const uint32_t *d_status, void *stream, int *status);
 
 /* ======================================================================
- * (4b) The other static codecs of src/codec.rs in bulk (exact 64-bit generic kernels, one lane
- *      per chunk; chunk c is one reference message from the initial message gen_kind / seed
- *      gives it, as in the _ex calls of section 4).  sym_bytes may also be 8 here.
+ * (4b) The other static codecs of src/codec.rs in bulk, one lane per chunk; chunk c is one
+ *      reference message from the initial message gen_kind / seed gives it, as in the _ex calls
+ *      of section 4.  sym_bytes may also be 8 here.  Fixed chunks whose symbols are whole 128-B
+ *      lines (chunk_len * sym_bytes % 128 == 0) run their full chunks on the fast kernels
+ *      (ans_mfast.hpp: LDS stream rings, f64 / magic-reciprocal division); the ragged last chunk,
+ *      variable chunks, other layouts and Independent sets beyond the fast range run on the
+ *      exact 64-bit kernels.  Both give the same bytes.
  *      A Categorical with norm >= 2^32 (up to 2^56) or more than 65536 symbols takes these
  *      kernels through the section-4 calls themselves (ans_gpu_table_create accepts it; its
  *      paths flags are 0; ans_dev_gen_iid / sample_iid return ANS_E_NORM_RANGE for it).
@@ -317,6 +321,39 @@ int ans_gpu_independent_encode_chunks(ans_gpu_tableset *ts, const uint32_t *tabl
 int ans_gpu_independent_decode_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const uint8_t *in,
                                       uint64_t in_len, const uint64_t *offsets, const uint64_t *lens, uint64_t n,
                                       uint64_t chunk_len, int gen_kind, uint64_t seed, void *out, int sym_bytes);
+/* 1 (fast kernels: every table has <= 256 symbols and norm in [2^16, 2^31], at most 31 tables),
+ * 2 (the same, with rows of near-certain symbols that take the voted exact renorm), 0 (exact only) */
+int ans_gpu_tableset_fast(const ans_gpu_tableset *ts, int *fast);
+
+/* Device-resident 4b calls (replace the bulk IID::push / pop and Independent::push / pop of
+ * src/codec.rs:388-399,415-424 on device memory): fixed chunks, chunk j's stream in its slot at
+ * d_slots + j*slot_cap (slot_cap from the _slot_capacity calls), lengths in d_lens, errors OR-ed
+ * into *d_status as (1u << status) bits (ans_dev_status); asynchronous on `stream` (NULL = the
+ * context's).  Decoders read slots (d_offsets NULL) or a dense container at d_in + d_offsets[j].
+ * d_tids: the table id of every position, one byte each (sets of at most 256 tables; ids are
+ * not range-checked on the device, as the reference would index past its codec vector). */
+int ans_gpu_uniform_slot_capacity(uint64_t size, uint64_t chunk_len, uint64_t *slot_cap);
+int ans_gpu_loguniform_slot_capacity(uint32_t excl_max_bits, uint64_t chunk_len, uint64_t *slot_cap);
+int ans_gpu_tableset_slot_capacity(const ans_gpu_tableset *ts, uint64_t chunk_len, uint64_t *slot_cap);
+int ans_dev_uniform_encode(ans_gpu *g, uint64_t size, const void *d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
+                           int gen_kind, uint64_t seed, uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens,
+                           uint32_t *d_status, void *stream);
+int ans_dev_uniform_decode(ans_gpu *g, uint64_t size, const uint8_t *d_in, const uint64_t *d_offsets, uint64_t slot_cap,
+                           const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
+                           void *d_syms, int sym_bytes, uint32_t *d_status, void *stream);
+int ans_dev_loguniform_encode(ans_gpu *g, uint32_t excl_max_bits, const void *d_syms, int sym_bytes, uint64_t n,
+                              uint64_t chunk_len, int gen_kind, uint64_t seed, uint8_t *d_slots, uint64_t slot_cap,
+                              uint32_t *d_lens, uint32_t *d_status, void *stream);
+int ans_dev_loguniform_decode(ans_gpu *g, uint32_t excl_max_bits, const uint8_t *d_in, const uint64_t *d_offsets,
+                              uint64_t slot_cap, const uint32_t *d_lens, uint64_t n, uint64_t chunk_len, int gen_kind,
+                              uint64_t seed, void *d_syms, int sym_bytes, uint32_t *d_status, void *stream);
+int ans_dev_independent_encode(ans_gpu_tableset *ts, const uint8_t *d_tids, const void *d_syms, int sym_bytes,
+                               uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed, uint8_t *d_slots,
+                               uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status, void *stream);
+int ans_dev_independent_decode(ans_gpu_tableset *ts, const uint8_t *d_tids, const uint8_t *d_in,
+                               const uint64_t *d_offsets, uint64_t slot_cap, const uint32_t *d_lens, uint64_t n,
+                               uint64_t chunk_len, int gen_kind, uint64_t seed, void *d_syms, int sym_bytes,
+                               uint32_t *d_status, void *stream);
 
 /* ======================================================================
  * (5) Graph models' bulk-IID caller — DenseSetIID<EdgeIndex, AllEdgeIndices> with an

@@ -97,6 +97,16 @@ SIGNATURES = {
     "ans_gpu_tableset_free": (None, [vp]),
     "ans_gpu_independent_encode_chunks": (ci, [vp, vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_independent_decode_chunks": (ci, [vp, vp, vp, u64, vp, vp, u64, u64, ci, u64, vp, ci]),
+    "ans_gpu_tableset_fast": (ci, [vp, ctypes.POINTER(ci)]),
+    "ans_gpu_uniform_slot_capacity": (ci, [u64, u64, ctypes.POINTER(u64)]),
+    "ans_gpu_loguniform_slot_capacity": (ci, [ctypes.c_uint32, u64, ctypes.POINTER(u64)]),
+    "ans_gpu_tableset_slot_capacity": (ci, [vp, u64, ctypes.POINTER(u64)]),
+    "ans_dev_uniform_encode": (ci, [vp, u64, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_uniform_decode": (ci, [vp, u64, vp, vp, u64, vp, u64, u64, ci, u64, vp, ci, vp, vp]),
+    "ans_dev_loguniform_encode": (ci, [vp, ctypes.c_uint32, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_loguniform_decode": (ci, [vp, ctypes.c_uint32, vp, vp, u64, vp, u64, u64, ci, u64, vp, ci, vp, vp]),
+    "ans_dev_independent_encode": (ci, [vp, vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_independent_decode": (ci, [vp, vp, vp, vp, u64, vp, u64, u64, ci, u64, vp, ci, vp, vp]),
     "ans_gpu_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_decode_chunks": (ci, [vp, vp, u64, vp, vp, u64, u64, ci, vp, ci]),
     "ans_dev_encode_chunks": (ci, [vp, vp, ci, u64, u64, vp, u64, vp, vp, vp]),
@@ -821,6 +831,25 @@ class GpuUniform:
         return out[:n]
 
 
+    # device-resident (include/ans_capi.h 4b): fixed chunks in slots, asynchronous on `stream`
+    def slot_capacity(self, chunk_len):
+        c = u64(0)
+        _check(lib().ans_gpu_uniform_slot_capacity(self.size, chunk_len, ctypes.byref(c)), "ans_gpu_uniform_slot_capacity")
+        return c.value
+
+    def dev_encode(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None,
+                   gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_uniform_encode(self.gpu.h, self.size, _dptr(d_syms), sym_bytes, n, chunk_len, gen_kind, seed,
+                                            _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_status), _sptr(stream)),
+               "ans_dev_uniform_encode")
+
+    def dev_decode(self, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status, stream=None,
+                   gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_uniform_decode(self.gpu.h, self.size, _dptr(d_in), _dptr(d_offsets), slot_cap,
+                                            _dptr(d_lens), n, chunk_len, gen_kind, seed, _dptr(d_syms), sym_bytes,
+                                            _dptr(d_status), _sptr(stream)), "ans_dev_uniform_decode")
+
+
 class GpuLogUniform:
     """IID<LogUniform::new(excl_max_bits)> in chunks on the GPU (src/codec.rs:561-611), the item
     of MaxBenfordIID (src/param_codec.rs:117-119)."""
@@ -848,6 +877,25 @@ class GpuLogUniform:
                                                       _np_ptr(out), _WIDTH[np.dtype(dtype)]),
                "ans_gpu_loguniform_decode_chunks")
         return out[:n]
+
+
+    def slot_capacity(self, chunk_len):
+        c = u64(0)
+        _check(lib().ans_gpu_loguniform_slot_capacity(self.excl_max_bits, chunk_len, ctypes.byref(c)),
+               "ans_gpu_loguniform_slot_capacity")
+        return c.value
+
+    def dev_encode(self, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None,
+                   gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_loguniform_encode(self.gpu.h, self.excl_max_bits, _dptr(d_syms), sym_bytes, n, chunk_len,
+                                               gen_kind, seed, _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_status),
+                                               _sptr(stream)), "ans_dev_loguniform_encode")
+
+    def dev_decode(self, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status, stream=None,
+                   gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_loguniform_decode(self.gpu.h, self.excl_max_bits, _dptr(d_in), _dptr(d_offsets), slot_cap,
+                                               _dptr(d_lens), n, chunk_len, gen_kind, seed, _dptr(d_syms), sym_bytes,
+                                               _dptr(d_status), _sptr(stream)), "ans_dev_loguniform_decode")
 
 
 class GpuTableSet:
@@ -891,6 +939,30 @@ class GpuTableSet:
                                                        gen_kind, seed, _np_ptr(out), _WIDTH[np.dtype(dtype)]),
                "ans_gpu_independent_decode_chunks")
         return out[:n]
+
+    def fast(self):
+        """1 / 2: the set runs on the fast kernels (2: with voted exact renorm rows); 0: exact only."""
+        f = ci(0)
+        _check(lib().ans_gpu_tableset_fast(self.h, ctypes.byref(f)), "ans_gpu_tableset_fast")
+        return f.value
+
+    def slot_capacity(self, chunk_len):
+        c = u64(0)
+        _check(lib().ans_gpu_tableset_slot_capacity(self.h, chunk_len, ctypes.byref(c)), "ans_gpu_tableset_slot_capacity")
+        return c.value
+
+    def dev_encode(self, d_tids, d_syms, sym_bytes, n, chunk_len, d_slots, slot_cap, d_lens, d_status, stream=None,
+                   gen_kind=GEN_ZEROS, seed=0):
+        """d_tids: one byte per position (device)."""
+        _check(lib().ans_dev_independent_encode(self.h, _dptr(d_tids), _dptr(d_syms), sym_bytes, n, chunk_len, gen_kind,
+                                                seed, _dptr(d_slots), slot_cap, _dptr(d_lens), _dptr(d_status),
+                                                _sptr(stream)), "ans_dev_independent_encode")
+
+    def dev_decode(self, d_tids, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, d_syms, sym_bytes, d_status,
+                   stream=None, gen_kind=GEN_ZEROS, seed=0):
+        _check(lib().ans_dev_independent_decode(self.h, _dptr(d_tids), _dptr(d_in), _dptr(d_offsets), slot_cap,
+                                                _dptr(d_lens), n, chunk_len, gen_kind, seed, _dptr(d_syms), sym_bytes,
+                                                _dptr(d_status), _sptr(stream)), "ans_dev_independent_decode")
 
 
 # ============================================================== graph models' bulk caller (section 5)

@@ -1,0 +1,880 @@
+// ans_mfast.hpp — throughput kernels for the codecs beside IID<Categorical> (included by
+// ans_codecs.hip): Independent<Categorical> (src/codec.rs:366-403) over a set of <= 256-symbol
+// tables staged in LDS, IID<Uniform(size)> (src/codec.rs:13-49) and IID<LogUniform(E)>
+// (src/codec.rs:561-611, the item of MaxBenfordIID, src/param_codec.rs:91-129).
+//
+// One lane = one chunk = one reference Message, exactly as in ans_fast.hpp, whose gfx950 idioms
+// these kernels reuse: global memory touched only at wave-uniform points (s_waitcnt vmcnt(0)),
+// whole 128-B lines per lane for symbols and stream pages, a per-lane [dword][lane] LDS ring
+// for the stream, byte funnels through v_alignbyte / v_perm, the f64 quotient estimate with a
+// voted exact fix-up.  What is new here is what these codecs need and IID<Categorical> does not:
+//
+//  * A model per codec (IndepModel, UniformModel, LogUniformModel below) supplies the per-symbol
+//    push and pop; the skeletons (k_menc, k_mdec) own the chunk walk, the ring and the pages.
+//  * 256-lane workgroups: the ring sits at LDS offset 0 (32 KiB encode, 33 KiB decode) and the
+//    model's tables after it, so an Independent set of several 256-symbol tables still leaves
+//    room for two workgroups per CU; 2^28 symbols in 4,096-symbol chunks (65,536 chains) then
+//    fill every CU with one workgroup each.
+//  * Codecs of different norms in one message (Independent, LogUniform's two Uniforms) make the
+//    reference's renorm bidirectional (src/ans.rs:233-253): a push may first take back a byte it
+//    pushed (renorm_up), a pop may hand one back (renorm_down).  Every head in the fast range is
+//    >= 2^55 after a push (norm * K > 2^56 - norm), so either move is at most ONE byte, and the
+//    stream position never falls more than one byte below its running maximum (encode) / rises
+//    more than one above its running minimum (decode).  The encoder therefore flushes a page
+//    only once the position is a byte past it (nothing flushed is ever taken back), and the
+//    decoder's page landing (P < 64 low + 60) already leaves the byte above the window in the
+//    ring.  Both moves are rare and run on wave-voted branches.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ans_fast.hpp"
+
+namespace shuffle_coding {
+namespace mfast {
+
+using fast::ab;
+using fast::ChunkInit;
+using fast::hi32;
+using fast::lds_ld128;
+using fast::lds_ld32;
+using fast::lds_ld64;
+using fast::lds_u32;
+using fast::lo32;
+using fast::mk64;
+using fast::shl16;
+using fast::unroll_seq;
+using fast::wait_vm;
+
+constexpr int kLanes = 256;                       // chunks per workgroup
+constexpr uint32_t kEncRingBytes = 32 * kLanes * 4;  // 128-B ring per lane: 32 KiB
+constexpr uint32_t kDecRows = 33;                 // 32 ring rows + the mirror of row 0
+constexpr uint32_t kDecRingBytes = kDecRows * kLanes * 4;  // 33 KiB
+constexpr uint32_t kEncTab = kEncRingBytes;       // LDS offset of the encoder's model tables
+constexpr uint32_t kDecTab = kDecRingBytes;       // LDS offset of the decoder's model tables
+static_assert(kDecTab % 256 == 0, "tables 256-B aligned");
+constexpr uint32_t kLdsMax = 160 * 1024;
+constexpr uint64_t kMaxMinHead = 1ull << 56;  // src/ans.rs:19
+
+// encoder error bits (lane-private; reported as ANS_E_* by the skeleton)
+constexpr uint32_t kErrSymbol = 1;    // symbol outside the alphabet (src/codec.rs:63, LogUniform bits >= size)
+constexpr uint32_t kErrZeroMass = 2;  // assert_ne!(p, 0) (src/ans.rs:98)
+constexpr uint32_t kErrNormRange = 4; // Uniform::new(2^(bits-1)) beyond MAX_SIZE (src/codec.rs:35)
+constexpr uint32_t kErrPulled = 8;    // a take-back reached past the stream's start (generator bytes)
+
+// ====================================================================== encoder
+// The stream's dword i lives in ring row i & 31: LDS ((i & 31) << 10) | 4 lane.
+struct MRing {
+    uint32_t col;
+    __device__ __forceinline__ lds_u32& at(int32_t i) const {
+        const uint32_t a = ((static_cast<uint32_t>(i) << 10) & 0x7C00u) | col;
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a));
+    }
+};
+
+// The byte funnel of ans_fast.hpp (FunnelT) on the 256-lane ring, plus take_back: pos8 = 8 *
+// stream bytes so far; X holds dword pos/4 with its pos&3 written bytes at the bottom; every
+// dword below it is in the ring.
+struct MFunnel {
+    uint32_t X, pos8, neg8, addr, col;
+
+    __device__ __forceinline__ void push(uint32_t lo, uint32_t k8) {
+        uint32_t xv, d0, d1;
+        asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
+        asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d0) : "v"(lo), "v"(pos8), "v"(xv));
+        asm("v_lshrrev_b32 %0, %1, %2" : "=v"(d1) : "v"(neg8), "v"(lo));
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = d0;
+        pos8 += k8;
+        neg8 -= k8;
+        const uint32_t a = (shl16<5>(pos8) & 0x7C00u) | col;  // ((pos8 >> 5) & 31) << 10
+        X = a != addr ? d1 : d0;
+        addr = a;
+    }
+    // the last byte back (renorm_up during a push, src/ans.rs:239-243); pos8 > 0
+    __device__ __forceinline__ uint32_t take_back() {
+        pos8 -= 8;
+        neg8 += 8;
+        const uint32_t a = (shl16<5>(pos8) & 0x7C00u) | col;
+        if (a != addr) {  // the byte lies in the dword below, which is in the ring
+            X = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a));
+            addr = a;
+        }
+        return (X >> (pos8 & 31u)) & 0xFFu;
+    }
+    __device__ __forceinline__ uint32_t len() const { return pos8 >> 3; }
+    __device__ __forceinline__ void finish() {
+        uint32_t xv;
+        asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = xv;
+    }
+};
+
+// completed pages leave in aligned 128-B pairs (ans_fast.hpp PageOut)
+struct MPageOut {
+    uint4 h0, h1, h2, h3;
+    __device__ __forceinline__ void page(const MRing& ring, uint32_t p, uint8_t* dst) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = ring.at(static_cast<int32_t>(16 * p + i));
+        const uint4 v0 = make_uint4(w[0], w[1], w[2], w[3]), v1 = make_uint4(w[4], w[5], w[6], w[7]);
+        const uint4 v2 = make_uint4(w[8], w[9], w[10], w[11]), v3 = make_uint4(w[12], w[13], w[14], w[15]);
+        if (p & 1) {
+            uint4* d = reinterpret_cast<uint4*>(dst + 64ull * (p - 1));
+            d[0] = h0;
+            d[1] = h1;
+            d[2] = h2;
+            d[3] = h3;
+            d[4] = v0;
+            d[5] = v1;
+            d[6] = v2;
+            d[7] = v3;
+        }
+        h0 = v0;
+        h1 = v1;
+        h2 = v2;
+        h3 = v3;
+    }
+    __device__ __forceinline__ void finish(uint32_t np, uint8_t* dst) {
+        if (np & 1) {
+            uint4* d = reinterpret_cast<uint4*>(dst + 64ull * (np - 1));
+            d[0] = h0;
+            d[1] = h1;
+            d[2] = h2;
+            d[3] = h3;
+        }
+    }
+};
+
+// One chain's encoder state, handed to the model's push.
+struct EncLane {
+    uint64_t head;
+    MFunnel f;
+    uint32_t err;
+    // push the head's low 8k8/8 bytes (up to 8) and drop them from the head
+    __device__ __forceinline__ void emit(uint32_t k8) {
+        f.push(lo32(head), min(k8, 32u));
+        if (k8 > 32u) f.push(hi32(head), k8 - 32u);
+        head >>= k8;
+    }
+    __device__ __forceinline__ void emit4(uint32_t k8) {  // at most 4 bytes
+        f.push(lo32(head), k8);
+        head >>= k8;
+    }
+    // renorm_up: head = head << 8 | last byte while head < bound (src/ans.rs:239-243); at most one
+    // byte for the fast range's heads, but exact whatever the count.  A take-back past the stream
+    // start reads the tail generator; a byte container cannot carry that (kErrPulled).
+    __device__ __forceinline__ void take_back_until(uint64_t bound) {
+        for (int g = 0; g < 8 && head < bound; ++g) {
+            uint32_t b = 0;
+            if (f.pos8 == 0) err |= kErrPulled;
+            else b = f.take_back();
+            head = (head << 8) | b;
+        }
+    }
+};
+
+// 8 * #{j >= 1 : head >> 8j >= pK} (src/ans.rs:246-253), exact (the voted slow paths)
+__device__ __forceinline__ uint32_t bytes_out8_exact(uint64_t head, uint64_t pK) {
+    uint32_t k = 0;
+    while (k < 7 && (head >> (8 * (k + 1))) >= pK) ++k;
+    return 8 * k;
+}
+
+// symbol j of a 16-B unit (u8 / u16 / u32 in the low bits; u64 as (lo, hi))
+template <typename Sym>
+__device__ __forceinline__ void unit_sym(const uint4& v, int j, uint32_t& lo, uint32_t& hi) {
+    if constexpr (sizeof(Sym) == 8) {
+        lo = j == 0 ? v.x : v.z;
+        hi = j == 0 ? v.y : v.w;
+    } else {
+        constexpr int per = 4 / static_cast<int>(sizeof(Sym));
+        const int wi = j / per, sh = 8 * static_cast<int>(sizeof(Sym)) * (j % per);
+        const uint32_t w = wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w;
+        lo = sizeof(Sym) == 4 ? w : (w >> sh) & ((1u << (8 * sizeof(Sym))) - 1u);
+        hi = 0;
+    }
+}
+template <typename Sym>
+__device__ __forceinline__ void unit_put(uint4& v, int j, uint32_t lo, uint32_t hi) {
+    if constexpr (sizeof(Sym) == 8) {
+        if (j == 0) {
+            v.x = lo;
+            v.y = hi;
+        } else {
+            v.z = lo;
+            v.w = hi;
+        }
+    } else {
+        constexpr int per = 4 / static_cast<int>(sizeof(Sym));
+        const int wi = j / per, sh = 8 * static_cast<int>(sizeof(Sym)) * (j % per);
+        uint32_t& w = wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w;
+        w = (j % per) == 0 ? lo : (w | (lo << sh));
+    }
+}
+
+// The encode skeleton.  Chunk c (< nfull: every chunk holds chunk_len symbols, chunk_len * w a
+// multiple of 128) is IID / Independent::push of its symbols last first (src/codec.rs:388-391,
+// 415-420) from the chunk's initial message, then flatten (src/ans.rs:255-260), into slot c.
+// Symbols (and table ids) come in 128-B groups per lane, walked last to first; a point (the
+// page flush) precedes every SPP symbols, which emit at most 64 bytes between them.
+template <class Model, typename Sym, int SPP>
+__global__ __launch_bounds__(kLanes, 2) void k_menc(Model md, const Sym* __restrict__ syms,
+                                                     const uint8_t* __restrict__ tids, uint64_t chunk_len,
+                                                     uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                     uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
+                                                     ChunkInit ini) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    md.stage_enc(lds + kEncTab);
+    __syncthreads();
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+    if (c >= nfull) return;
+
+    constexpr int U = 16 / static_cast<int>(sizeof(Sym));  // symbols per 16-B unit
+    static_assert(U % SPP == 0 || SPP % U == 0, "points split units evenly");
+    constexpr int GU = 8;                                    // units per 128-B group
+    constexpr int GS = GU * U;                               // symbols per group
+    constexpr int TB = GS;                                   // table-id bytes per group
+    const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
+    const uint8_t* tsrc = Model::kTids ? tids + c * chunk_len : nullptr;
+    uint8_t* dst = slots + c * slot_cap;
+    const uint32_t npages_cap = static_cast<uint32_t>(slot_cap / 64);
+    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
+
+    const MRing ring{4 * threadIdx.x};
+    MPageOut pout;
+    EncLane e;
+    e.head = ini.head(c);  // Message::zeros() / random(seed + c)
+    e.f = MFunnel{0, 0, 0, ring.col, ring.col};
+    e.err = 0;
+    uint32_t fp = 0, over = 0;
+    // page fp leaves once the position is a byte past it: a take-back never reaches a flushed page
+    auto flush_ready = [&]() __attribute__((always_inline)) {
+        if (e.f.pos8 >= 512u * fp + 520u) {
+            if (fp < npages_cap) pout.page(ring, fp, dst);
+            else over = 1;
+            ++fp;
+        }
+    };
+
+    uint4 n[GU], tn[GU];
+#pragma unroll
+    for (int i = 0; i < GU; ++i) {
+        n[i] = make_uint4(0, 0, 0, 0);
+        tn[i] = make_uint4(0, 0, 0, 0);
+    }
+    auto load_group = [&](int g) __attribute__((always_inline)) {
+        const uint4* gs = src + GU * g;
+#pragma unroll
+        for (int i = 0; i < GU; ++i) n[i] = gs[i];
+        if constexpr (Model::kTids) {
+            const uint4* gt = reinterpret_cast<const uint4*>(tsrc + static_cast<uint64_t>(TB) * g);
+#pragma unroll
+            for (int i = 0; i < TB / 16; ++i) tn[i] = gt[i];
+        }
+    };
+    if (ngroups > 0) load_group(ngroups - 1);
+    for (int g = ngroups - 1; g >= 0; --g) {
+        uint4 cc[GU], tc[GU];
+#pragma unroll
+        for (int i = 0; i < GU; ++i) {
+            cc[i] = n[i];
+            tc[i] = tn[i];
+        }
+        auto unit = [&](auto ic) __attribute__((always_inline)) {
+            constexpr int u = GU - 1 - decltype(ic)::value;  // last unit first
+            if (u == GU / 2 - 1 && g > 0) load_group(g - 1);
+#pragma unroll
+            for (int j = U - 1; j >= 0; --j) {  // last symbol first (src/codec.rs:417)
+                if ((j + 1) % SPP == 0 || j == U - 1) flush_ready();
+                __builtin_amdgcn_sched_barrier(0);
+                // the symbol's words pass a volatile fence first, so that their unpacking stays
+                // at the push (hoisted to the group's start, the unpacked symbols of a whole
+                // group were held in registers and spilled)
+                uint4 cv = cc[u];
+                if constexpr (sizeof(Sym) == 8) {
+                    if (j == 0) asm volatile("" : "+v"(cv.x), "+v"(cv.y));
+                    else asm volatile("" : "+v"(cv.z), "+v"(cv.w));
+                } else {
+                    const int wi = j / (4 / static_cast<int>(sizeof(Sym)));  // (folded: j is unrolled)
+                    if (wi == 0) asm volatile("" : "+v"(cv.x));
+                    else if (wi == 1) asm volatile("" : "+v"(cv.y));
+                    else if (wi == 2) asm volatile("" : "+v"(cv.z));
+                    else asm volatile("" : "+v"(cv.w));
+                }
+                uint32_t lo, hi;
+                unit_sym<Sym>(cv, j, lo, hi);
+                uint32_t tid = 0;
+                if constexpr (Model::kTids) {
+                    const int tb = u * U + j;  // table-id byte of this symbol within the group
+                    const uint4& tv = tc[tb / 16];
+                    const int wi = (tb % 16) / 4;
+                    uint32_t w = wi == 0 ? tv.x : wi == 1 ? tv.y : wi == 2 ? tv.z : tv.w;
+                    asm volatile("" : "+v"(w));
+                    tid = (w >> (8 * (tb % 4))) & 0xFFu;
+                }
+                md.push(e, lo, hi, tid);
+            }
+        };
+        unroll_seq(unit, std::make_integer_sequence<int, GU>{});
+    }
+    flush_ready();  // the flatten's 8 bytes then stay within the page after the held one
+
+    // flatten (src/ans.rs:255-260): all significant head bytes, low first (7 or 8: head > 2^55)
+    const uint32_t nb = (71u - static_cast<uint32_t>(__builtin_clzll(e.head))) >> 3;
+    e.f.push(lo32(e.head), 32);
+    e.f.push(hi32(e.head), 8 * (nb - 4));
+    e.f.finish();
+    const uint32_t len = e.f.len();
+    for (const uint32_t last = (len + 63) / 64; fp < last; ++fp) {
+        if (fp < npages_cap) pout.page(ring, fp, dst);
+        else over = 1;
+    }
+    if (!over) pout.finish(fp, dst);
+    uint32_t err = e.err;
+    if (err & kErrZeroMass) err = md.classify(syms + c * chunk_len, tsrc, chunk_len, err);
+    if (err) {
+        const int code = (err & kErrSymbol) ? ANS_E_SYMBOL : (err & kErrNormRange) ? ANS_E_NORM_RANGE
+                         : (err & kErrZeroMass) ? ANS_E_ZERO_MASS : ANS_E_MISMATCH;
+        atomicOr(status, 1u << code);
+    }
+    if (over) atomicOr(status, 1u << ANS_E_LEN);
+    lens[c] = (over || err) ? 0u : len;
+}
+
+// ====================================================================== decoder
+// The ans_fast.hpp DecChain on a 256-lane ring at LDS offset 0 (33 rows, row 32 mirrors row 0),
+// plus the renorm_down (push-back) of the bidirectional renorm and the two-round pull of codecs
+// whose pops can take more than four bytes (Uniform and LogUniform sizes up to 2^46).
+__device__ const uint4 kZeroPair[8] = {};  // the Zeros tail generator's bytes below a stream
+
+struct MChain {
+    const uint8_t* src;
+    uint4 Q[8];
+    int32_t low, P8, lim8;
+    uint32_t W, wx, wy, col;
+    uint64_t head;
+    bool bad;  // a pushed-back byte that differs from the stream's: corrupt (ANS_E_MISMATCH)
+
+    template <int R0>
+    __device__ __forceinline__ uint32_t put_half(uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
+        const uint32_t base = col + R0 * kLanes * 4;
+        asm volatile(
+            "ds_write2st64_b32 %0, %1, %2 offset0:0 offset1:4\n\t"
+            "ds_write2st64_b32 %0, %3, %4 offset0:8 offset1:12\n\t"
+            "ds_write2st64_b32 %0, %5, %6 offset0:16 offset1:20\n\t"
+            "ds_write2st64_b32 %0, %7, %8 offset0:24 offset1:28\n\t"
+            "ds_write2st64_b32 %0, %9, %10 offset0:32 offset1:36\n\t"
+            "ds_write2st64_b32 %0, %11, %12 offset0:40 offset1:44\n\t"
+            "ds_write2st64_b32 %0, %13, %14 offset0:48 offset1:52\n\t"
+            "ds_write2st64_b32 %0, %15, %16 offset0:56 offset1:60"
+            :
+            : "v"(base), "v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+              "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w)
+            : "memory");
+        return a0.x;
+    }
+    __device__ __forceinline__ void put_page(int32_t p) {
+        if (p & 1) {
+            put_half<16>(Q[4], Q[5], Q[6], Q[7]);
+        } else {
+            const uint32_t r0 = put_half<0>(Q[0], Q[1], Q[2], Q[3]);
+            *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(col + 32u * kLanes * 4)) = r0;  // mirror
+        }
+    }
+    __device__ __forceinline__ void fetch_pair(int32_t m) {
+        typedef __attribute__((address_space(1), aligned(1))) const fast::v4u32 gv4;
+        const uint4* g = m >= 0 ? reinterpret_cast<const uint4*>(src + 128ll * m) : kZeroPair;
+        const gv4* gg = reinterpret_cast<const gv4*>(reinterpret_cast<uintptr_t>(g));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const fast::v4u32 v = gg[k];
+            Q[k] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    }
+    // the top pair as the aligned dwords holding stream bytes (no read past the stream's line)
+    __device__ __forceinline__ void fetch_top(int32_t m, int32_t len) {
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src) + 128ll * m;
+        const gu32* d0 = reinterpret_cast<const gu32*>(a & ~uintptr_t(3));
+        const uint32_t b = static_cast<uint32_t>(a & 3u);
+        const int32_t last = static_cast<int32_t>(((reinterpret_cast<uintptr_t>(src) + len - 1) >> 2) - (a >> 2));
+        uint32_t d[33];
+#pragma unroll
+        for (int q = 0; q < 33; ++q) d[q] = q <= last ? d0[q] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            Q[k] = make_uint4(ab(d[4 * k + 1], d[4 * k], b), ab(d[4 * k + 2], d[4 * k + 1], b),
+                              ab(d[4 * k + 3], d[4 * k + 2], b), ab(d[4 * k + 4], d[4 * k + 3], b));
+    }
+    // W = stream bytes [P, P+4): ring rows (P>>2)&31 and the next; P8 = 8P
+    __device__ __forceinline__ void read_window() {
+        uint32_t a;
+        asm("v_lshl_or_b32 %0, %1, 5, %2" : "=v"(a) : "v"(static_cast<uint32_t>(P8) & 0x3E0u), "v"(col));
+        wy = lds_ld32(a);
+        wx = lds_ld32(a + 4 * kLanes);
+    }
+    __device__ __forceinline__ void form_window() { W = __builtin_amdgcn_alignbit(wx, wy, static_cast<uint32_t>(P8)); }
+    __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
+        src = s;
+        bad = false;
+        const int32_t top = len > 0 ? (len - 1) >> 6 : 0;
+        if (len > 0) fetch_top(top >> 1, len);
+        else fetch_pair(-1);
+        wait_vm();
+        put_page(top);
+        if (top & 1) {
+            put_page(top - 1);
+            fetch_pair((top >> 1) - 1);
+        } else {
+            fetch_pair((top >> 1) - 1);
+            wait_vm();
+            put_page(top - 1);
+        }
+        low = top - 1;
+        lim8 = 8 * (64 * low + 60);
+        P8 = 8 * (len - 4);
+        read_window();
+        head = 0;
+    }
+    __device__ __forceinline__ void pull_until(uint64_t bound) {
+        for (int g = 0; g < 9 && head < bound; ++g) {
+            form_window();
+            head = (head << 8) | (W >> 24);
+            P8 -= 8;
+            read_window();
+        }
+    }
+    __device__ __forceinline__ void point() {
+        if (P8 < lim8) {
+            put_page(low - 1);
+            --low;
+            lim8 -= 512;
+            if (!(low & 1)) fetch_pair((low >> 1) - 1);
+        }
+    }
+    // renorm(L) (src/ans.rs:233-253) from the window W: head = head << 8k | the top k bytes of W for
+    // the least k in 0..4 that reaches L (ans_fast.hpp renorm_up8: byte permutes from the clz),
+    // or, when head >> 8 >= L already (a codec of a smaller L before this one), renorm_down: the
+    // head's low byte goes back onto the stream (P moves up one byte), where it must equal the
+    // stream's own byte (checked against the ring; a mismatch is a corrupt stream).  Both rare
+    // cases sit behind one 32-bit screen voted per wave.  Returns the bits the position moves down.
+    __device__ __forceinline__ int32_t renorm_up8(uint64_t L, uint32_t hL8) {
+        const uint32_t h1 = hi32(head), h0 = lo32(head);
+        uint32_t fb;
+        asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
+        const uint32_t m = min(fb, 32u) & 0x38u;  // 8 js
+        const uint32_t sel = hi32(0x0706050403020100ull << m);
+        const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
+        head = mk64(xj1, xj0);
+        int32_t m8 = static_cast<int32_t>(m);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(xj1 >= hL8) != 0, 0)) {
+            const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
+            if (xj1 >= hL8 && mk64(xm1, xm0) >= L) {
+                head = mk64(xm1, xm0);
+                m8 -= 8;
+                if (m == 0) {  // renorm_down: byte xj0 & 0xFF back onto the stream at P + 4
+                    const int32_t p8 = P8 + 32;
+                    uint32_t a;
+                    asm("v_lshl_or_b32 %0, %1, 5, %2" : "=v"(a) : "v"(static_cast<uint32_t>(p8) & 0x3E0u), "v"(col));
+                    const uint32_t byte = (lds_ld32(a) >> (static_cast<uint32_t>(p8) & 31u)) & 0xFFu;
+                    bad |= byte != (xj0 & 0xFFu);
+                }
+            }
+        }
+        return m8;
+    }
+    // renorm to L for heads that may need more than four bytes (a second round, voted)
+    __device__ __forceinline__ void renorm_wide(uint64_t L, uint32_t hL8) {
+        form_window();
+        P8 -= renorm_up8(L, hL8);
+        read_window();
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(head < L) != 0, 0)) {
+            if (head < L) {
+                form_window();
+                P8 -= renorm_up8(L, hL8);
+                read_window();
+            }
+        }
+    }
+};
+
+// The decode skeleton: chunk c's stream read from its end (Tail::pop, src/ans.rs:198-203),
+// unflatten (src/ans.rs:262-264), then IID / Independent::pop forward (src/codec.rs:393-399,
+// 422-424); the symbols leave in whole 128-B lines; at the end the message must be back at the
+// chunk's initial one (src/ans.rs:56).  A point precedes every SPP symbols (at most 60 stream
+// bytes between points, so no window read reaches an unlanded page).
+template <class Model, typename Sym, int SPP>
+__global__ __launch_bounds__(kLanes, 2) void k_mdec(Model md, const uint8_t* __restrict__ slots, uint64_t slot_cap,
+                                                     const uint64_t* __restrict__ offsets,
+                                                     const uint32_t* __restrict__ lens,
+                                                     const uint8_t* __restrict__ tids, uint64_t chunk_len,
+                                                     uint64_t nfull, int gen_kind, Sym* __restrict__ out,
+                                                     uint32_t* __restrict__ status, ChunkInit ini) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    md.stage_dec(lds + kDecTab);
+    __syncthreads();
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+    if (c >= nfull) return;
+
+    constexpr int U = 16 / static_cast<int>(sizeof(Sym));
+    static_assert(U % SPP == 0 || SPP % U == 0, "points split units evenly");
+    const int nunit = static_cast<int>(chunk_len / U);  // chunk_len * w is a multiple of 128: whole lines
+    uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
+    const uint8_t* tsrc = Model::kTids ? tids + c * chunk_len : nullptr;
+
+    if ((!offsets && lens[c] > slot_cap) || lens[c] >= (1u << 27)) {
+        atomicOr(status, 1u << ANS_E_LEN);
+        return;
+    }
+    MChain ch;
+    ch.col = 4 * threadIdx.x;
+    ch.start(slots + (offsets ? offsets[c] : c * slot_cap), static_cast<int32_t>(lens[c]));
+    ch.pull_until(md.first_bound(tsrc));  // Message::unflatten: head 0, the first pop's renorm_up
+    typename Model::DecState ds;
+    md.dec_init(ds);
+
+    // the table ids of the unit being decoded and of the next (requested a unit ahead)
+    uint4 tcur = make_uint4(0, 0, 0, 0), tnext = make_uint4(0, 0, 0, 0);
+    if constexpr (Model::kTids) tcur = *reinterpret_cast<const uint4*>(tsrc);
+    uint4 q[8];
+    for (int u0 = 0; u0 < nunit; u0 += 8) {
+        auto unit = [&](auto ic) __attribute__((always_inline)) {
+            constexpr int uu = decltype(ic)::value;
+            const int u = u0 + uu;
+            uint4 outv = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                if (j % SPP == 0) {
+                    wait_vm();  // point
+                    if (j == 0 && uu == 0 && u0 > 0) {
+                        uint4* d = dst + (u0 - 8);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) d[k] = q[k];
+                    }
+                    if (j == 0 && Model::kTids) {
+                        if (uu > 0 || u0 > 0) tcur = tnext;
+                        if (u + 1 < nunit) {
+                            const int tb = (u + 1) * U;  // first table-id byte of the next unit
+                            tnext = make_uint4(0, 0, 0, 0);
+                            if constexpr (U == 16) tnext = *reinterpret_cast<const uint4*>(tsrc + tb);
+                            else if constexpr (U == 8) {
+                                const uint2 v = *reinterpret_cast<const uint2*>(tsrc + tb);
+                                tnext = make_uint4(v.x, v.y, 0, 0);
+                            } else if constexpr (U == 4) {
+                                tnext = make_uint4(*reinterpret_cast<const uint32_t*>(tsrc + tb), 0, 0, 0);
+                            } else {
+                                tnext = make_uint4(*reinterpret_cast<const uint16_t*>(tsrc + tb), 0, 0, 0);
+                            }
+                        }
+                    }
+                    ch.point();
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                uint32_t tid = 0;
+                if constexpr (Model::kTids) {
+                    const int wi = j / 4;
+                    const uint32_t w = wi == 0 ? tcur.x : wi == 1 ? tcur.y : wi == 2 ? tcur.z : tcur.w;
+                    tid = (w >> (8 * (j % 4))) & 0xFFu;
+                }
+                uint32_t hi = 0;
+                uint32_t lo = md.pop(ch, ds, tid, hi);
+                // the symbol is formed here (volatile fences keep their order): otherwise the
+                // compiler sank every pop's symbol arithmetic to the line's store and kept its
+                // operands (the table header among them) alive across 128 pops, in scratch
+                if constexpr (sizeof(Sym) == 8) asm volatile("" : "+v"(lo), "+v"(hi));
+                else asm volatile("" : "+v"(lo));
+                unit_put<Sym>(outv, j, lo, hi);
+            }
+            asm volatile("" : "+v"(outv.x), "+v"(outv.y), "+v"(outv.z), "+v"(outv.w));
+            q[uu] = outv;
+        };
+        unroll_seq(unit, std::make_integer_sequence<int, 8>{});
+    }
+    wait_vm();
+    if (nunit > 0) {  // the last line (nunit is a multiple of 8: chunk bytes % 128 == 0)
+        uint4* d = dst + (nunit - 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = q[k];
+    }
+    // assert_eq!(initial, m) (src/ans.rs:56, 302-310)
+    ch.pull_until(kMaxMinHead);
+    const int32_t remaining = (ch.P8 >> 3) + 4;  // < 0: generated
+    if (remaining < 0 && gen_kind == ANS_GEN_EMPTY) atomicOr(status, 1u << ANS_E_EXHAUSTED);
+    else if (ch.bad || md.dec_bad(ds) || ch.head != ini.head(c) || remaining != 0) atomicOr(status, 1u << ANS_E_MISMATCH);
+}
+
+// ====================================================================== helpers for the models
+// floor(x / d) for any u64 x and 1 <= d < 2^64, from m = floor((2^64 - 1) / d): the product's
+// high word is q or q - 1 (m >= 2^64/d - 1), one compare fixes it.  r = x - q d.
+__device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
+__device__ __forceinline__ uint64_t div_magic(uint64_t x, uint64_t d, uint64_t m, uint64_t& r) {
+    uint64_t q = mulhi64(x, m);
+    r = x - q * d;
+    if (r >= d) {
+        ++q;
+        r -= d;
+    }
+    return q;
+}
+
+// stage `bytes` (a multiple of 16) of a global image into LDS (every thread of the workgroup)
+__device__ __forceinline__ void stage_image(const uint4* __restrict__ g, uint32_t bytes, unsigned char* l) {
+    uint4* d = reinterpret_cast<uint4*>(l);
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += kLanes) d[i] = g[i];
+}
+
+struct NoState {
+    __device__ __forceinline__ bool bad() const { return false; }
+};
+
+// ====================================================================== Independent<Categorical>
+// A set of T <= kIndMaxTables Categoricals with <= 256 symbols and norm in [2^16, 2^31]
+// (src/codec.rs:51-92), a table per position (src/codec.rs:366-403), table ids as one byte each.
+//
+// Encoder image (LDS kEncTab, the same bytes in global memory): row (t, s) at t*8224 + 32 s,
+// s < 257 (s >= nsym: zero mass), then K_t (u64) per table at k_off.  A row is
+//   {rcp = 1/p (f64), p, cdf(s), w, norm, screen}
+// read as two ds_read_b128.  w is the renorm word: every push starts from head in
+// [Hmin, 2^64) (Hmin = min_t norm_t K_t > 2^56 - 2^31, or the chunk's initial head), where the
+// bounds pK 2^8j (src/ans.rs:246-253) below Hmin always count, and with T = the first above it,
+// k = k0 + [head >= T] whenever 2^8 T >= 2^64: w = T + 8 k0 (T's low byte is zero), one compare
+// as in ans_renorm.hpp.  Rows where that fails (2^8 T < 2^64, or pK = 2^56), or where a push can
+// start below pK and take a byte back (pK > Hmin: a symbol of probability above 1 - 2^-25), get
+// a screen: hi32(head) <= screen sends the lane to the exact renorm on a voted branch (kRare;
+// sets without such rows compile it out).
+//
+// Decoder image (LDS kDecTab): a 32-B header per table at t*32 {1/norm (f64), L = norm K (u64),
+// norm, hL8 (the renorm screen), LDS address of bucket 0, us | rshift << 8 | 8*257*t << 16}, the
+// (cdf(s), pmf(s)) rows of every table at kIndRowOff + 8 (t*257 + s), then each table's icdf
+// buckets of width 2^us (ans_fast.hpp kModeU's folded words): bucket j at a = j << us holds
+// w1 = ((min(cdf(s0+1) - a, 2^us) - 1) << rshift) | s0 and w2 the same for cdf(s0+2) with bit 9
+// set when cdf(s0+3) still lies inside the bucket (a voted scan of the rows handles cf beyond
+// s0+2 there).  rshift = 32 - us >= 10 keeps the 9-bit symbol clear, so a table of norm 2^31
+// needs only 512 buckets.
+constexpr uint32_t kIndRowBytes = 32;
+constexpr uint32_t kIndTabStride = 257 * kIndRowBytes;  // 8224
+constexpr uint32_t kIndMaxTables = 31;                  // 32-B headers in 1 KiB, row offsets in 16 bits
+constexpr uint32_t kIndRowOff = 1024;                   // decoder rows after the headers
+constexpr uint32_t kIndFarBit = 0x200u;
+constexpr uint32_t kIndMaxShift = 22;                   // rshift = 32 - us >= 10
+
+template <bool kRare>
+struct IndepModel {
+    static constexpr bool kTids = true;
+    using DecState = NoState;
+    const uint4* enc_img;
+    const uint4* dec_img;
+    const uint32_t* nsym;  // per table, global (error classification)
+    uint32_t enc_bytes, dec_bytes, k_off;
+
+    __device__ __forceinline__ void stage_enc(unsigned char* l) const { stage_image(enc_img, enc_bytes, l); }
+    __device__ __forceinline__ void stage_dec(unsigned char* l) const { stage_image(dec_img, dec_bytes, l); }
+
+    // blanket push (src/ans.rs:96-105) with Categorical t's row (src/codec.rs:63-64)
+    __device__ __forceinline__ void push(EncLane& e, uint32_t sym, uint32_t, uint32_t tid) const {
+        const uint32_t off = kEncTab + __umul24(tid, kIndTabStride) + (min(sym, 256u) << 5);
+        const uint4 ra = lds_ld128(off), rb = lds_ld128(off + 16);
+        const double rcp = __longlong_as_double(static_cast<long long>(mk64(ra.y, ra.x)));
+        const uint32_t mass = ra.z, cum = ra.w, norm = rb.z;
+        const uint64_t w = mk64(rb.y, rb.x);
+        uint32_t k8 = (rb.x & 0xFFu) + (mk64(hi32(e.head), lo32(e.head) | 0xFFu) > w ? 8u : 0u);
+        if constexpr (kRare) {
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(hi32(e.head) <= rb.w) != 0, 0)) {
+                if (hi32(e.head) <= rb.w) {  // exact renorm(pK): take back, then count (src/ans.rs:233-253)
+                    const uint64_t pK = static_cast<uint64_t>(mass) * lds_ld64(kEncTab + k_off + 8 * tid);
+                    e.take_back_until(pK);
+                    k8 = bytes_out8_exact(e.head, pK);
+                }
+            }
+        }
+        e.emit4(k8);
+        // q = head / p, r = head % p (src/ans.rs:101-102): round(head/p - 1/2), exact unless head/p
+        // lies within 2^-4 of an integer; such lanes (and zero-mass rows, rcp 0) take the voted
+        // 64-bit remainder (ans_fast.hpp k_encode push_one)
+        uint64_t qb = fast::qest_half(e.head, rcp);
+        uint32_t rm = lo32(e.head) - lo32(qb) * mass;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= mass) != 0, 0)) {
+            if (rm >= mass) {
+                if (mass == 0) e.err |= kErrZeroMass;
+                const int64_t r = static_cast<int64_t>(e.head - (qb - 0x4330000000000000ull) * mass);
+                const int64_t d = r < 0 ? -1 : 1;
+                qb += static_cast<uint64_t>(d);
+                rm = static_cast<uint32_t>(r - d * static_cast<int64_t>(mass));
+            }
+        }
+        // head = norm * q + cdf(x, r) (src/ans.rs:103-104): q < 2^52, hi32(q) = the raw high word's
+        // low 20 bits
+        const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * norm + (cum + rm);
+        e.head = mk64(hi32(lo64) + (hi32(qb) & 0xFFFFFu) * norm, lo32(lo64));
+    }
+    // a zero-mass lane: an out-of-range symbol (src/codec.rs:63) or p == 0 (src/ans.rs:98)
+    template <typename Sym>
+    __device__ uint32_t classify(const Sym* s, const uint8_t* t, uint64_t len, uint32_t err) const {
+        for (uint64_t k = 0; k < len; ++k)
+            if (static_cast<uint32_t>(s[k]) >= nsym[t[k]]) return err | kErrSymbol;
+        return err;
+    }
+
+    __device__ __forceinline__ uint64_t first_bound(const uint8_t* t) const {
+        return lds_ld64(kDecTab + 32 * t[0] + 8);
+    }
+    __device__ __forceinline__ void dec_init(DecState&) const {}
+    __device__ __forceinline__ bool dec_bad(const DecState&) const { return false; }
+    // blanket pop (src/ans.rs:107-116) with Categorical t's icdf (src/codec.rs:65-68)
+    __device__ __forceinline__ uint32_t pop(MChain& ch, DecState&, uint32_t tid, uint32_t& hi) const {
+        // (a volatile fence on the table id: the header reads of a unit's pops are not hoisted
+        // ahead of the pops before them, which held every header in registers at once)
+        asm volatile("" : "+v"(tid));
+        const uint32_t ha = kDecTab + shl16<5>(tid);
+        const uint4 h0 = lds_ld128(ha), h1 = lds_ld128(ha + 16);
+        const double rcp_norm = __longlong_as_double(static_cast<long long>(mk64(h0.y, h0.x)));
+        const uint64_t L = mk64(h0.w, h0.z);
+        const uint32_t norm = h1.x, hL8 = h1.y, bkt = h1.z;
+        const uint32_t us = h1.w & 0xFFu, rsh = (h1.w >> 8) & 0xFFu, rows = h1.w >> 16;  // rows: 8 * 257 t
+        ch.form_window();
+        ch.P8 -= ch.renorm_up8(L, hL8);
+        ch.read_window();  // for the next pop
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t qq;
+        uint32_t cf;
+        fast::div_norm(ch.head, norm, rcp_norm, qq, cf);
+        const uint64_t cc = lds_ld64(bkt + ((cf >> us) << 3));
+        const uint32_t rx = cf << rsh;
+        uint32_t sx;
+        asm volatile(
+            "v_cmp_gt_u32 vcc, %[rx], %[w1]\n\t"
+            "s_nop 1\n\t"
+            "v_addc_co_u32 %[sx], vcc, 0, %[w1], vcc\n\t"
+            "v_cmp_gt_u32 vcc, %[rx], %[w2]\n\t"
+            "s_nop 1\n\t"
+            "v_addc_co_u32 %[sx], vcc, 0, %[sx], vcc"
+            : [sx] "=&v"(sx)
+            : [rx] "v"(rx), [w1] "v"(lo32(cc)), [w2] "v"(hi32(cc))
+            : "vcc");
+        sx &= 0x1FFu;  // the symbol (w1's threshold bits above it dropped)
+        const bool far = (hi32(cc) & kIndFarBit) && rx > hi32(cc);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(far) != 0, 0)) {
+            if (far) {  // three or more boundaries in the bucket: scan the rows past s0 + 2
+                while (cf >= lo32(lds_ld64(kDecTab + kIndRowOff + rows + 8 * (sx + 1)))) ++sx;
+            }
+        }
+        uint32_t ra;
+        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(sx), "v"(rows));
+        const uint64_t row = lds_ld64(kDecTab + kIndRowOff + ra);  // (cdf(s), pmf(s))
+        // head = pmf(s) q + cf - cdf(s) (src/ans.rs:113-114)
+        ch.head = qq * hi32(row) + (cf - lo32(row));
+        hi = 0;
+        return sx;
+    }
+};
+
+// ====================================================================== IID<Uniform(size)>
+// size <= MAX_SIZE = 2^46 (src/codec.rs:13-49): pmf 1, cdf(x, 0) = x.  A push is renorm(K) and
+// head = size * head + x (no division); one codec, so every push starts in [L, 2^8 L) and the
+// renorm is ans_renorm.hpp's one-compare word (up to 7 bytes).  A pop is renorm(L) (two rounds
+// of up to four bytes when size > 2^24) and (q, x) = head divmod size: a shift for powers of
+// two, else the high word of head * floor((2^64 - 1) / size) and one fix-up.
+template <bool kPow2>
+struct UniformModel {
+    static constexpr bool kTids = false;
+    using DecState = NoState;
+    uint64_t size, K, L, w, magic;
+    uint32_t log2size, hL8;
+
+    __device__ __forceinline__ void stage_enc(unsigned char*) const {}
+    __device__ __forceinline__ void stage_dec(unsigned char*) const {}
+    __device__ __forceinline__ void push(EncLane& e, uint32_t lo, uint32_t hi, uint32_t) const {
+        const uint64_t x = mk64(hi, lo);
+        if (x >= size) e.err |= kErrSymbol;  // outside the alphabet (the reference would code garbage)
+        const uint32_t k8 = (lo32(w) & 0xFFu) + (mk64(hi32(e.head), lo32(e.head) | 0xFFu) > w ? 8u : 0u);
+        e.emit(k8);
+        e.head = kPow2 ? ((e.head << log2size) | x) : size * e.head + x;
+    }
+    template <typename Sym>
+    __device__ uint32_t classify(const Sym*, const uint8_t*, uint64_t, uint32_t err) const { return err; }
+    __device__ __forceinline__ uint64_t first_bound(const uint8_t*) const { return L; }
+    __device__ __forceinline__ void dec_init(DecState&) const {}
+    __device__ __forceinline__ bool dec_bad(const DecState&) const { return false; }
+    __device__ __forceinline__ uint32_t pop(MChain& ch, DecState&, uint32_t, uint32_t& hi) const {
+        ch.renorm_wide(L, hL8);
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t x;
+        if constexpr (kPow2) {
+            x = ch.head & (size - 1);
+            ch.head >>= log2size;
+        } else {
+            ch.head = div_magic(ch.head, size, magic, x);
+        }
+        hi = hi32(x);
+        return lo32(x);
+    }
+};
+
+// ====================================================================== IID<LogUniform(E)>
+// (src/codec.rs:561-611) Per element x: bits = 64 - clz(x) (0 for x = 0), a Uniform(2^(bits-1))
+// push of x's bits below the top one (K = 2^(57 - bits): renorm by bit lengths, the head shifted
+// up by bits - 1), then a Uniform(E + 1) push of bits (at most one byte out: its K >= 2^49.9).
+// Only bits = 1 can take a byte back (Uniform(1): bound 2^56); only the bits pop can hand one
+// back (MChain::renorm_up8).  The pop is the mirror: renorm(L_E) in up to two rounds,
+// (head, bits) = head divmod (E + 1) by the magic reciprocal, then renorm(2^56) and the low bits.
+struct LogUniformState {
+    bool bad;
+};
+struct LogUniformModel {
+    static constexpr bool kTids = false;
+    using DecState = LogUniformState;
+    uint64_t nb, KE, LE, TEm1, magic;  // TEm1 = 2^8 KE - 1 (~0 when E = 0: no byte ever)
+    uint32_t hL8E;
+
+    __device__ __forceinline__ void stage_enc(unsigned char*) const {}
+    __device__ __forceinline__ void stage_dec(unsigned char*) const {}
+    __device__ __forceinline__ void push(EncLane& e, uint32_t lo, uint32_t hi, uint32_t) const {
+        const uint64_t x = mk64(hi, lo);
+        const uint32_t bits = x ? 64u - static_cast<uint32_t>(__builtin_clzll(x)) : 0u;  // LogUniform::get_bits
+        if (bits >= nb) e.err |= kErrSymbol;                                               // assert!(bits < size)
+        else if (bits > 47) e.err |= kErrNormRange;  // Uniform::new(2^(bits-1)) > MAX_SIZE
+        if (bits != 0) {
+            // Uniform(2^(bits-1)) push of the low bits: renorm(2^s), s = 57 - bits
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits == 1 && e.head < kMaxMinHead) != 0, 0)) {
+                if (bits == 1) e.take_back_until(kMaxMinHead);
+            }
+            const uint32_t bl = 64u - static_cast<uint32_t>(__builtin_clzll(e.head));
+            const int32_t t = static_cast<int32_t>(bl) - static_cast<int32_t>(58u - min(bits, 48u));
+            e.emit(t > 0 ? 8u * (static_cast<uint32_t>(t) >> 3) : 0u);
+            const uint32_t sh = min(bits, 48u) - 1u;
+            e.head = (e.head << sh) | (x & ((1ull << sh) - 1ull));
+        }
+        // Uniform(E + 1) push of bits: one byte out iff head >= 2^8 KE
+        e.emit4(e.head > TEm1 ? 8u : 0u);
+        e.head = e.head * nb + bits;
+    }
+    template <typename Sym>
+    __device__ uint32_t classify(const Sym*, const uint8_t*, uint64_t, uint32_t err) const { return err; }
+    __device__ __forceinline__ uint64_t first_bound(const uint8_t*) const { return LE; }
+    __device__ __forceinline__ void dec_init(DecState& s) const { s.bad = false; }
+    __device__ __forceinline__ bool dec_bad(const DecState& s) const { return s.bad; }
+    __device__ __forceinline__ uint32_t pop(MChain& ch, DecState& st, uint32_t, uint32_t& hi) const {
+        ch.renorm_wide(LE, hL8E);
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t bits64;
+        ch.head = div_magic(ch.head, nb, magic, bits64);
+        const uint32_t bits = lo32(bits64);
+        uint64_t x = 0;
+        if (bits != 0) {
+            st.bad |= bits > 47;  // no valid stream holds such a count (the encoder refuses it)
+            ch.form_window();
+            ch.P8 -= ch.renorm_up8(kMaxMinHead, 0xFFFFFFFFu);  // renorm(2^(bits-1) * 2^(57-bits)) = 2^56
+            ch.read_window();
+            const uint32_t sh = min(bits, 48u) - 1u;
+            x = (ch.head & ((1ull << sh) - 1ull)) | (1ull << sh);
+            ch.head >>= sh;
+        }
+        hi = hi32(x);
+        return lo32(x);
+    }
+};
+
+}  // namespace mfast
+}  // namespace shuffle_coding
