@@ -146,6 +146,8 @@ void ans_gpu_table_free(ans_gpu_table *gt);
 #define ANS_PATH_DEC_U 256u     /* LDS decoder without the quotient fix-up (u-domain tables): applies to
                                   * sym_bytes == 1 only; u16 / u32 decodes of the same table run the
                                   * row decoder (kModeRows: the same bytes, one fix-up more) */
+#define ANS_PATH_ENC_SHIFT 512u /* packed large-alphabet encoder whose renorm reads a shift byte per
+                                  * mass (every mass <= 4096) instead of comparing bit lengths */
 int ans_gpu_table_paths(const ans_gpu_table *gt, uint32_t *paths);
 /* worst-case stream bytes of one chunk of chunk_len symbols, rounded up to 16 */
 int ans_gpu_slot_capacity(const ans_gpu_table *gt, uint64_t chunk_len, uint64_t *slot_cap);

@@ -31,6 +31,7 @@ ANS_PATH_ENC_WIDE, ANS_PATH_DEC_WIDE = 16, 32
 ANS_PATH_DEC_COMPACT = 64
 ANS_PATH_ENC_PACKED = 128
 ANS_PATH_DEC_U = 256
+ANS_PATH_ENC_SHIFT = 512
 MAX_MIN_HEAD = 1 << 56
 MAX_SIZE = MAX_MIN_HEAD >> 10
 

@@ -35,9 +35,10 @@ constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 // encode LDS rows: rcp[257], (mass, cum)[257] and the first renorm threshold
 // thr[257] = p*K*2^8 - 1 (saturated at 2^64 - 1); the others follow from it (k_encode)
-constexpr uint32_t kEncMcOffset = 8 * 257;
-constexpr uint32_t kEncThrOffset = 2 * kEncMcOffset;
-constexpr uint32_t kEncLdsBytes = (3 * kEncMcOffset + 15) & ~15u;
+// LDS-row encoder tables at offset 0: rcp (8 B per symbol) at 0, then 16-B rows
+// {mass, cum, renorm word} at kEncRowOffset (row of symbol s at kEncRowOffset + 16 s)
+constexpr uint32_t kEncRowOffset = (8 * 257 + 15) & ~15u;
+constexpr uint32_t kEncLdsBytes = kEncRowOffset + 16 * 257;
 constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB
 // encode LDS: the row tables at offset 0 (a row address is the symbol times 8, each array at an
 // immediate offset), the ring after them at a multiple of 256 B (the ds_write2st64 offset unit),
@@ -364,12 +365,13 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                                                                          const uint32_t* __restrict__ vlen = nullptr) {
     static_assert(!(kVar && kGlobalRows), "staged chunks take the LDS-row kernel");
     extern __shared__ __align__(16) unsigned char lds[];
-    // rows split into two 8-byte arrays (rcp | mass,cum): a wave's random row reads then spread
-    // over all 64 banks (ds_read_b64, 32-lane groups) instead of 16 bank quads (16-byte rows)
-    // rows at offset 0, ring after them (kEncRingBase)
+    // a symbol's row is two random LDS reads: rcp by ds_read_b64 (32-lane groups over 32 bank
+    // pairs) and {mass, cum, renorm word} by one ds_read_b128 (16-lane groups over 16 bank
+    // quads).  Three 8-B arrays read by three ds_read_b64 cost ~1.1x the LDS cycles for random
+    // rows (expected worst bank load 3.9 of 32 lanes vs 3.3 of 16) and one more instruction.
+    // Tables at offset 0, ring after them (kEncRingBase)
     double* rcps = reinterpret_cast<double*>(lds);
-    uint2* mcs = reinterpret_cast<uint2*>(lds + kEncMcOffset);  // immediate ds offset from rcps
-    uint64_t* thrs = reinterpret_cast<uint64_t*>(lds + kEncThrOffset);
+    uint4* rows = reinterpret_cast<uint4*>(lds + kEncRowOffset);
     // u8 symbols index the rows unclamped: all 256 byte values get a row (zero mass beyond the
     // alphabet, so they fail like the sentinel row they used to be clamped to)
     constexpr bool kByteRows = sizeof(Sym) == 1;
@@ -377,8 +379,8 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         const uint32_t nrows = kByteRows ? 256u : t.enc_rows;
         for (uint32_t i = threadIdx.x; i < nrows; i += kBlock) {
             const EncRow r = i < t.enc_rows ? t.enc[i] : EncRow{0.0, 0u, 0u};
-            mcs[i] = make_uint2(r.mass, r.cum);
-            thrs[i] = enc_thr(static_cast<uint64_t>(r.mass) * t.K, t.L);
+            const uint64_t w = enc_thr(static_cast<uint64_t>(r.mass) * t.K, t.L);
+            rows[i] = make_uint4(r.mass, r.cum, lo32(w), hi32(w));
             rcps[i] = r.rcp;  // 0 for zero mass: such a push always takes the voted branch
         }
     }
@@ -388,10 +390,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         uint64_t thr;
     };
     auto row_at = [&](uint32_t off) __attribute__((always_inline)) {  // off = 8 * symbol (tables at LDS offset 0)
-        const uint64_t mc = lds_ld64(off + kEncMcOffset);
+        const uint4 v = lds_ld128(shl16<1>(off) + kEncRowOffset);  // 16 * symbol < 2^16
         Row r;
-        r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(mc), hi32(mc)};
-        r.thr = lds_ld64(off + kEncThrOffset);
+        r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), v.x, v.y};
+        r.thr = mk64(v.w, v.z);
         return r;
     };
     const Ring ring{4 * threadIdx.x};

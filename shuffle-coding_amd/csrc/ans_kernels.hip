@@ -410,8 +410,21 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     // the packed prefix (ans_table.hpp enc_pack): the longest multiple of 16 symbols whose image
     // fits the same LDS and whose in-block offsets fit u16; used when it is longer
     std::vector<uint32_t> pack_img;
+    uint32_t pmax = 0;
+    for (uint32_t s = 0; s < nsym; ++s) pmax = std::max<uint32_t>(pmax, static_cast<uint32_t>(cat.masses[s]));
+    // k_encode_w<kSa> (ans_wide.hpp): a renorm shift byte per mass 0..pmax at LDS offset 0, when
+    // every mass has one (ans_renorm.hpp enc_sa); it takes kWideSaBytes from the prefix
+    std::vector<uint8_t> sa_img;
+    if (ft.enc_wide && pmax <= fast::kWideSaMax) {
+        sa_img.assign(fast::kWideSaBytes, 8);
+        for (uint32_t p = 0; p <= pmax && !sa_img.empty(); ++p) {
+            const uint32_t sa = fast::enc_sa(static_cast<uint64_t>(p) * t.K, t.L);
+            if (sa == 0) sa_img.clear();
+            else sa_img[p] = static_cast<uint8_t>(sa);
+        }
+    }
     if (ft.enc_wide) {
-        const uint32_t budget = 4 * fast::kWideEncCumMax;
+        const uint32_t budget = 4 * fast::kWideEncCumMax - (sa_img.empty() ? 0 : fast::kWideSaBytes);
         auto img_bytes = [](uint32_t nl) {
             const uint32_t ooff = 4 * ((nl >> 4) + 2);
             return (ooff + 2 * (nl + 2) + 3) & ~3u;
@@ -436,8 +449,10 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             ft.enc_nl = nlp;
             ft.enc_pack_ooff = ooff;
             ft.enc_pack_bytes = img_bytes(nlp);
+            ft.enc_sa = sa_img.empty() ? 0 : 1;
         }
     }
+    if (!ft.enc_sa) sa_img.clear();
     // k_decode_w's LDS prefix: for each bucket width 2^shp, the longest prefix of symbols whose
     // bucket starts (u16) and cdf fit beside the ring; keep the width whose prefix covers the most
     // probability among those whose cf needs a fifth candidate at most 0.1% of the time
@@ -499,8 +514,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_cum_off = fast::kDecCumOff;
     ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;
-    ft.pmax = 0;
-    for (uint32_t s = 0; s < nsym; ++s) ft.pmax = std::max<uint32_t>(ft.pmax, static_cast<uint32_t>(cat.masses[s]));
+    ft.pmax = pmax;
     ft.K = t.K;
     ft.L = t.L;
     ft.rcp_norm = t.rcp_norm;
@@ -514,7 +528,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const size_t decc_b = sizeof(DecBucketC) * decc.size();
     const size_t o_pack = o_decc + ((decc_b + 255) & ~size_t(255));
     const size_t pack_b = sizeof(uint32_t) * pack_img.size();
-    const size_t o_uimg = o_pack + ((pack_b + 255) & ~size_t(255));
+    const size_t o_sa = o_pack + ((pack_b + 255) & ~size_t(255));
+    const size_t o_uimg = o_sa + ((sa_img.size() + 255) & ~size_t(255));
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
     HIP_TRY(hipMalloc(&mem, o_uimg + uimg.size() + 16));
@@ -537,6 +552,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dbkt_c = reinterpret_cast<const DecBucketC*>(base + o_decc);
     if (pack_b) HIP_TRY(hipMemcpy(base + o_pack, pack_img.data(), pack_b, hipMemcpyHostToDevice));
     ft.enc_pack_img = reinterpret_cast<const uint32_t*>(base + o_pack);
+    if (!sa_img.empty()) HIP_TRY(hipMemcpy(base + o_sa, sa_img.data(), sa_img.size(), hipMemcpyHostToDevice));
+    ft.enc_sa_img = reinterpret_cast<const uint32_t*>(base + o_sa);
     if (!uimg.empty()) HIP_TRY(hipMemcpy(base + o_uimg, uimg.data(), uimg.size(), hipMemcpyHostToDevice));
     ft.dec_u_img = reinterpret_cast<const uint32_t*>(base + o_uimg);
     ft.dec_w_s0 = reinterpret_cast<const uint16_t*>(base + o_ws0);
@@ -1362,6 +1379,7 @@ int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
     if (ft.usable && ft.dec_wide) p |= ANS_PATH_DEC_WIDE;
     if (ft.usable && ft.dec_wide && ft.dec_c) p |= ANS_PATH_DEC_COMPACT;
     if (ft.usable && ft.enc_wide && ft.enc_pack) p |= ANS_PATH_ENC_PACKED;
+    if (ft.usable && ft.enc_wide && ft.enc_sa) p |= ANS_PATH_ENC_SHIFT;
     if (ft.usable && ft.dec_usable && !ft.dec_far && ft.dec_u) p |= ANS_PATH_DEC_U;
     *paths = p;
     return ANS_OK;

@@ -297,6 +297,11 @@ __global__ __launch_bounds__(kBlock) void k_span_lens(ChunkSpan<Sym> span, uint6
 
 constexpr int kNotStaged = -2;
 
+// dynamic LDS of k_encode_w: the shift table (kSa), the ring and the prefix image
+inline size_t wide_enc_lds(const FastTable& ft) {
+    return (ft.enc_sa ? fast::kWideSaBytes : 0) + fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
+}
+
 // The staged route applies to the large-alphabet fast kernels (u16 / u32 symbols).
 template <typename Sym>
 bool staged_encode_ok(const ans_gpu_table* gt) {  // large-alphabet or LDS-row encoder
@@ -328,19 +333,15 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
         k_stage<Sym><<<grid_for(units), kBlock, 0, s>>>(syms, span, nchunks, lpad, stage, vlen);
         const unsigned grid = static_cast<unsigned>((nchunks + fast::kBlock - 1) / fast::kBlock);
         const bool k32 = ft.K < (1ull << 32);
-        const size_t wlds = fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
+        const size_t wlds = wide_enc_lds(ft);
         // (u8 symbols never take the large-alphabet kernels: not instantiated for them)
         bool wide = false;
         if constexpr (sizeof(Sym) > 1) wide = ft.enc_wide;
         if (wide) {
             if constexpr (sizeof(Sym) > 1) {
-#define ENCV2(KM, K32, PK) fast::k_encode_w<Sym, KM, K32, PK, true><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
-#define ENCV(KM, K32) if (ft.enc_pack) ENCV2(KM, K32, true); else ENCV2(KM, K32, false)
-            switch (ft.kmax) {
-            case 1: case 2: if (k32) ENCV(2, true); else ENCV(2, false); break;
-            case 3: if (k32) ENCV(3, true); else ENCV(3, false); break;
-            default: if (k32) ENCV(4, true); else ENCV(4, false); break;
-            }
+#define ENCV2(K32, PK, SA) fast::k_encode_w<Sym, K32, PK, SA, true><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
+#define ENCV(K32) if (ft.enc_sa) ENCV2(K32, true, true); else if (ft.enc_pack) ENCV2(K32, true, false); else ENCV2(K32, false, false)
+            if (k32) ENCV(true); else ENCV(false);
 #undef ENCV
 #undef ENCV2
             }
@@ -470,14 +471,10 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         }
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
-                const size_t wlds = fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
-#define ENCW2(KM, K32, PK) fast::k_encode_w<Sym, KM, K32, PK><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
-#define ENCW(KM, K32) if (ft.enc_pack) ENCW2(KM, K32, true); else ENCW2(KM, K32, false)
-                switch (ft.kmax) {
-                case 1: case 2: if (k32) ENCW(2, true); else ENCW(2, false); break;
-                case 3: if (k32) ENCW(3, true); else ENCW(3, false); break;
-                default: if (k32) ENCW(4, true); else ENCW(4, false); break;
-                }
+                const size_t wlds = wide_enc_lds(ft);
+#define ENCW2(K32, PK, SA) fast::k_encode_w<Sym, K32, PK, SA><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+#define ENCW(K32) if (ft.enc_sa) ENCW2(K32, true, true); else if (ft.enc_pack) ENCW2(K32, true, false); else ENCW2(K32, false, false)
+                if (k32) ENCW(true); else ENCW(false);
 #undef ENCW
 #undef ENCW2
             } else if (ft.enc_global) {

@@ -27,5 +27,18 @@ constexpr uint64_t enc_thr(uint64_t pK, uint64_t L) {
     return L < (1ull << 56) ? (L << 8) : ~0xFFull;         // p = norm: never
 }
 
+// The same test as a shift of pK (the large-alphabet encoder, ans_wide.hpp k_encode_w<kSa>, which
+// has no per-symbol LDS row but a byte per MASS): with w = enc_thr(pK, L), T = pK << sa and
+// k = sa/8 - 1 + [head >= T] for sa = 8 + (w & 0xFF), in all three cases above (T = 2^8 A,
+// A = pK << 8 k0: sa = 8 (k0 + 1); A = L: T = A, sa = 8 k0; p = norm: T = L << 8 = pK << 8).
+// Returns 0 where no such shift exists (the caller then keeps the bit-length renorm).
+constexpr uint32_t enc_sa(uint64_t pK, uint64_t L) {
+    if (pK == 0) return 8;  // zero mass: the push is recorded as an error, any k will do
+    const uint64_t w = enc_thr(pK, L);
+    const uint32_t sa = 8 + static_cast<uint32_t>(w & 0xFF);
+    if (sa >= 64 || (pK << sa) >> sa != pK || (pK << sa) != (w & ~0xFFull)) return 0;
+    return sa;
+}
+
 }  // namespace fast
 }  // namespace shuffle_coding

@@ -116,6 +116,11 @@ struct FastTable {
     uint32_t enc_pack;
     uint32_t enc_pack_ooff;
     uint32_t enc_pack_bytes;  // image bytes (a multiple of 4), staged into LDS as u32 words
+    // k_encode_w<kSa> (every mass <= fast::kWideSaMax, with the packed prefix): the renorm shift
+    // of each mass, sa(p) = 8 (k0(p) + 1) with T = p*K << sa(p) (ans_renorm.hpp enc_sa), one
+    // byte per mass at LDS offset 0 (fast::kWideSaBytes, staged from enc_sa_img)
+    const uint32_t* enc_sa_img;
+    uint32_t enc_sa;
     // k_decode_w past the prefix: compact buckets (dec_c) of width 2^dec_c_shift, else dbkt_g
     const DecBucketC* dbkt_c;
     uint32_t dec_c;

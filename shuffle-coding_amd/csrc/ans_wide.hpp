@@ -24,11 +24,21 @@
 namespace shuffle_coding {
 namespace fast {
 
-// ---- encoder LDS: the byte ring at offset 0 (64 KiB, 512 lanes), the cdf prefix after it
+// ---- encoder LDS: the byte ring at offset 0 (64 KiB, 512 lanes), the cdf prefix after it.
+// kSa kernels put the per-mass renorm shifts first (kWideSaBytes at offset 0, so a shift's
+// address is the mass itself) and the ring and the prefix kWideSaBytes higher.
 constexpr uint32_t kWideRing = 0;
 constexpr uint32_t kWideEncCum = kEncRingBytes;
 constexpr uint32_t kWideEncCumMax = (160u * 1024u - kWideEncCum) / 4u;  // staged cdf entries
 constexpr uint32_t kWideNormMin = 1u << 22;  // one Newton step suffices above (see k_encode_w)
+constexpr uint32_t kWideSaMax = 4096;        // largest mass with a shift byte (12-bit masses)
+constexpr uint32_t kWideSaBytes = 4352;      // (kWideSaMax + 1) bytes, rounded up to 256
+static_assert(kWideSaBytes >= kWideSaMax + 1 && kWideSaBytes % 256 == 0, "shift table");
+template <bool kSa>
+struct WideEncLds {
+    static constexpr uint32_t ring = kSa ? kWideSaBytes : kWideRing;
+    static constexpr uint32_t cum = ring + kEncRingBytes;  // the prefix image
+};
 
 typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -62,24 +72,36 @@ __device__ __forceinline__ double rcp_newton(uint32_t p) {
 // kPack: the LDS prefix is the packed image (FastTable::enc_pack): a row costs a ds_read2_b32
 // of two block bases and two ds_read_u16 of offsets plus ~6 VALU, for ~1.8x the prefix (67%
 // of C4's symbols instead of 37%; the rest is the L2 request each).
+// kSa: every mass is at most kWideSaMax (FastTable::enc_sa) and its renorm shift sa(p) is one
+// LDS byte at address p: k = sa/8 - 1 + [head >= p*K << sa] (ans_renorm.hpp enc_sa), one 64-bit
+// shift and compare where the bit-length renorm takes three v_ffbh, two v_min, four adds, the
+// shift and the compare.  The unit's eight shift bytes are read before its first push.
 // kVar: chunk c holds vlen[c] <= chunk_len symbols at the start of its chunk_len-symbol stride
 // (a staged ragged or variable-length chunk, ans_kernels.hip launch_staged): its last group is
 // partial, and it is the first one coded, so the pushes past vlen[c] are skipped there.
-template <typename Sym, int KMAX, bool kK32, bool kPack, bool kVar = false>
+// (A push emits at most 4 bytes whatever the table, and the renorm never loops over j, so the
+// kernel has no KMAX parameter: one unit of 8 u16 / 4 u32 symbols completes at most one page.)
+template <typename Sym, bool kK32, bool kPack, bool kSa, bool kVar = false>
 __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
                                                          uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                          uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
                                                          ChunkInit ini, const uint32_t* __restrict__ vlen = nullptr) {
+    static_assert(!kSa || kPack, "the shift table comes with the packed prefix");
+    using Lay = WideEncLds<kSa>;
     extern __shared__ __align__(16) unsigned char lds[];
     {
-        uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideEncCum);
+        uint32_t* lc = reinterpret_cast<uint32_t*>(lds + Lay::cum);
         if constexpr (kPack) {
             for (uint32_t i = threadIdx.x; i < t.enc_pack_bytes / 4; i += kBlock) lc[i] = t.enc_pack_img[i];
         } else {
             for (uint32_t i = threadIdx.x; i <= t.enc_nl; i += kBlock) lc[i] = t.cum[i];
         }
+        if constexpr (kSa) {
+            uint32_t* ls = reinterpret_cast<uint32_t*>(lds);
+            for (uint32_t i = threadIdx.x; i < kWideSaBytes / 4; i += kBlock) ls[i] = t.enc_sa_img[i];
+        }
     }
-    const RingT<kWideRing> ring{4 * threadIdx.x};
+    const RingT<Lay::ring> ring{4 * threadIdx.x};
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= nfull) return;
@@ -100,8 +122,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     const uint32_t* gcum = t.cum;
 
     uint64_t head = ini.head(c);  // Message::zeros() / random(seed + c)
-    FunnelT<kWideRing> f{0, 0, 0, ring.col, ring.col};
-    PageOut<kWideRing> pout;
+    FunnelT<Lay::ring> f{0, 0, 0, ring.col, ring.col};
+    PageOut<Lay::ring> pout;
     uint32_t fp = 0, over = 0;
     uint32_t minmass = ~0u;
 
@@ -117,19 +139,19 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     // shared destination would make each LDS read wait for every outstanding global load)
     // (packed: lbuf holds the two block bases and the two offsets, combined in process)
     using LRow = typename std::conditional<kPack, uint4, v2u32>::type;
-    const uint32_t ooff = kWideEncCum + t.enc_pack_ooff;
+    const uint32_t ooff = Lay::cum + t.enc_pack_ooff;
     auto request = [&](const uint4& unit, LRow* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
             const uint32_t sp = umin(s, nl);
             if constexpr (kPack) {
-                const v2u32 b = cum_pair_lds(kWideEncCum, sp >> 4);
+                const v2u32 b = cum_pair_lds(Lay::cum, sp >> 4);
                 const uint32_t oa = ooff + 2 * sp;
                 lbuf[j] = make_uint4(b.x, b.y, *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa)),
                                      *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa + 2)));
             } else {
-                lbuf[j] = cum_pair_lds(kWideEncCum, sp);
+                lbuf[j] = cum_pair_lds(Lay::cum, sp);
             }
             if (s >= nl) gbuf[j] = cum_pair_global(gcum, s);
         }
@@ -156,17 +178,38 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         const uint32_t m8 = (clz_pk - fh + 7u) & ~7u;  // 8 * ceil(d / 8)
         return (head >> m8) >= pK ? m8 : m8 - 8u;
     };
+    // the row of symbol j of a unit: cdf(x), pmf(x) (src/codec.rs:63-64)
+    auto row_of = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, int j) __attribute__((always_inline)) {
+        const uint32_t sj = umin(sym_of<Sym>(unit, j), nsym);
+        const bool in_lds = sj < nl;
+        const v2u32 row = in_lds ? lrow(lbuf[j], sj) : gbuf[j];
+        return v2u32{row.x, row.y - row.x};
+    };
     auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, uint32_t upos) __attribute__((always_inline)) {
+        // kSa: the unit's rows and shift bytes first (p <= kWideSaMax: the byte at LDS address p)
+        v2u32 rows[U];
+        uint32_t sas[U];
+        if constexpr (kSa) {
+#pragma unroll
+            for (int j = U - 1; j >= 0; --j) {
+                rows[j] = row_of(unit, lbuf, gbuf, j);
+                sas[j] = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(rows[j].y));
+            }
+        }
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
-            const uint32_t sj = umin(sym_of<Sym>(unit, j), nsym);
-            const bool in_lds = sj < nl;
-            const v2u32 row = in_lds ? lrow(lbuf[j], sj) : gbuf[j];
-            const uint32_t cum = row.x, p = row.y - row.x;  // cdf(x), pmf(x) (src/codec.rs:63-64)
+            const v2u32 row = kSa ? rows[j] : row_of(unit, lbuf, gbuf, j);
+            const uint32_t cum = row.x, p = row.y;
             asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(p));
             const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
-            const uint32_t k8 = bytes_out8(pK);
+            uint32_t k8;
+            if constexpr (kSa) {
+                const uint32_t sa = sas[j];
+                k8 = head >= (pK << sa) ? sa : sa - 8u;
+            } else {
+                k8 = bytes_out8(pK);
+            }
             f.push(lo32(head), k8);
             head >>= k8;
             // q = head / p, r = head % p (src/ans.rs:101-102), head = norm*q + cdf(x, r)

@@ -790,22 +790,28 @@ def _wide_table(rng, nsym, lo, hi, ones=0, zeros=0, crowd=0):
     return masses.astype(np.uint64)
 
 
-@pytest.mark.parametrize("nsym,lo,hi,ones,zeros,crowd,chunk_len,n,compact,packed", [
-    (65536, 1, 1 << 12, 0, 0, 0, 4096, 600 * 4096 + 77, True, True),   # C4's shape, ragged tail
-    (65536, 1, 1 << 12, 300, 500, 20, 4096, 520 * 4096, True, True),  # kmax 4, zero masses, crowded buckets
-    (3000, 1 << 10, 1 << 13, 10, 0, 5, 64, 1200 * 64, True, False),    # small chunks (one 128-B group)
-    (40000, 1, 1 << 16, 0, 0, 0, 2048, 600 * 2048, False, False),     # prefix and global parts both
-])                                                                      # large; offsets past u16
-def test_wide_kernels_bit_exact(gpu, nsym, lo, hi, ones, zeros, crowd, chunk_len, n, compact, packed):
+@pytest.mark.parametrize("nsym,lo,hi,ones,zeros,crowd,chunk_len,n,compact,packed,shift", [
+    (65536, 1, 1 << 12, 0, 0, 0, 4096, 600 * 4096 + 77, True, True, True),   # C4's shape, ragged tail
+    (65536, 1, 1 << 12, 300, 500, 20, 4096, 520 * 4096, True, True, True),  # kmax 4, zero masses, crowded buckets
+    (3000, 1 << 10, 1 << 13, 10, 0, 5, 64, 1200 * 64, True, False, False),   # small chunks (one 128-B group)
+    (40000, 1, 1 << 16, 0, 0, 0, 2048, 600 * 2048, False, False, False),    # prefix and global parts both
+                                                                            # large; offsets past u16
+    (40000, 1, 5000, 0, 0, 0, 4096, 300 * 4096, None, True, False),         # packed, masses past the shift table
+    (50000, 1, 1 << 12, 2000, 0, 0, 1024, 900 * 1024, None, True, True),    # shift table, many unit masses
+])
+def test_wide_kernels_bit_exact(gpu, nsym, lo, hi, ones, zeros, crowd, chunk_len, n, compact, packed, shift):
     """The large-alphabet kernels (k_encode_w: cdf-pair rows from the LDS prefix or global
-    memory, 1/p by v_rcp_f64 + Newton; k_decode_w: LDS-prefix icdf + global buckets) against
-    the oracle, symbols drawn from the table so both table parts and the scans are hit."""
+    memory, 1/p by v_rcp_f64 + Newton, the renorm by bit lengths or by the per-mass shift byte;
+    k_decode_w: LDS-prefix icdf + global buckets) against the oracle, symbols drawn from the
+    table so both table parts and the scans are hit."""
     rng = np.random.default_rng(nsym + n)
     masses = _wide_table(rng, nsym, lo, hi, ones, zeros, crowd)
     gt = A.GpuTable(gpu, A.Categorical(masses))
     assert gt.paths() & A.ANS_PATH_ENC_WIDE and gt.decode_kernel(2) == "wide"
-    assert bool(gt.paths() & A.ANS_PATH_DEC_COMPACT) == compact
+    if compact is not None:
+        assert bool(gt.paths() & A.ANS_PATH_DEC_COMPACT) == compact
     assert bool(gt.paths() & A.ANS_PATH_ENC_PACKED) == packed
+    assert bool(gt.paths() & A.ANS_PATH_ENC_SHIFT) == shift
     nz = np.flatnonzero(masses)
     p = masses[nz].astype(np.float64)
     # half the symbols by probability, half uniform over the non-zero ones (tiny masses too)

@@ -1,5 +1,6 @@
-"""The LDS-row encoder's one-compare renorm (shuffle-coding_amd/csrc/ans_renorm.hpp enc_thr,
-DESIGN.md §3.1) against the reference's renorm loop, on the CPU.
+"""The fast encoders' one-compare renorms (shuffle-coding_amd/csrc/ans_renorm.hpp: the LDS-row
+encoder's word enc_thr, DESIGN.md §3.1, and the large-alphabet encoder's per-mass shift enc_sa,
+§3.3) against the reference's renorm loop, on the CPU.
 
 The reference pushes a symbol of mass p after `renorm(p * K)` (src/ans.rs:100), whose
 renorm_down emits head's low byte while `head >> 8 >= p * K` (src/ans.rs:246-253).  The kernel
@@ -9,7 +10,8 @@ of Message::zeros / empty (2^56) and Message::random ([2^56, 2^57), src/ans.rs:2
 test compiles a brute-force checker with g++ against the product header and compares the rule
 with the reference loop over random tables (norms 2^16..2^31, masses from 1 to norm) and heads
 drawn uniformly, next to the interval ends, within a few units of every bound p*K*2^8j, and
-from the initial-head range.
+from the initial-head range.  The shift rule k = sa/8 - 1 + [head >= p*K << sa] is checked on
+the same heads wherever enc_sa gives a shift (every table but the off-path p = norm, L = 2^56).
 """
 import os
 import subprocess
@@ -23,6 +25,7 @@ CHECKER = r"""
 #include <random>
 #include "ans_renorm.hpp"
 using shuffle_coding::fast::enc_thr;
+using shuffle_coding::fast::enc_sa;
 typedef unsigned __int128 u128;
 
 static uint32_t ref_k(uint64_t head, uint64_t pK) {  // src/ans.rs:246-253
@@ -33,11 +36,14 @@ static uint32_t ref_k(uint64_t head, uint64_t pK) {  // src/ans.rs:246-253
 static uint32_t kernel_k(uint64_t head, uint64_t w) {  // ans_fast.hpp k_encode bytes_out_w8
     return (uint32_t)((w & 0xFF) + ((head | 0xFF) > w ? 8 : 0)) / 8;
 }
+static uint32_t shift_k(uint64_t head, uint64_t pK, uint32_t sa) {  // ans_wide.hpp k_encode_w<kSa>
+    return (head >= (pK << sa) ? sa : sa - 8) / 8;
+}
 
 int main(int argc, char** argv) {
     std::mt19937_64 R(12345);
     const int tables = argc > 1 ? atoi(argv[1]) : 50000;
-    long n = 0, bad = 0, skipped = 0;
+    long n = 0, bad = 0, skipped = 0, nsa = 0;
     for (int it = 0; it < tables; ++it) {
         const int nb = 16 + (int)(R() % 16);
         uint64_t norm = (1ull << nb) + (R() % 3 == 0 ? 0 : R() % (1ull << nb));
@@ -54,6 +60,8 @@ int main(int argc, char** argv) {
         if (p > norm) p = norm;
         if (p == norm && L == (1ull << 56)) { ++skipped; continue; }  // kept off the fast path
         const uint64_t pK = p * K, w = enc_thr(pK, L);
+        const uint32_t sa = enc_sa(pK, L);
+        if (sa == 0) { ++bad; printf("no shift norm=%llu p=%llu\n", (unsigned long long)norm, (unsigned long long)p); }
         const u128 top = (u128)L << 8;  // the heads of every push: [L, 2^8 L)
         for (int h = 0; h < 48; ++h) {
             uint64_t head;
@@ -78,18 +86,26 @@ int main(int argc, char** argv) {
                 if (bad < 5) printf("bad norm=%llu p=%llu head=%llx\n", (unsigned long long)norm, (unsigned long long)p, (unsigned long long)head);
                 ++bad;
             }
+            if (sa) {
+                ++nsa;
+                if (shift_k(head, pK, sa) != ref_k(head, pK)) {
+                    if (bad < 5) printf("bad shift norm=%llu p=%llu head=%llx\n", (unsigned long long)norm, (unsigned long long)p, (unsigned long long)head);
+                    ++bad;
+                }
+            }
         }
         // initial heads: Message::zeros / empty (2^56) and Message::random, [2^56, 2^57)
         for (int h = 0; h < 8; ++h) {
             const uint64_t head = h == 0 ? (1ull << 56) : (1ull << 56) | (R() >> 8);
             if (head < L || (u128)head >= top) { ++bad; printf("initial head outside [L, 2^8 L)\n"); }
             ++n;
-            if (kernel_k(head, w) != ref_k(head, pK)) {
+            if (kernel_k(head, w) != ref_k(head, pK) || (sa && shift_k(head, pK, sa) != ref_k(head, pK))) {
                 if (bad < 5) printf("bad initial head norm=%llu p=%llu head=%llx\n", (unsigned long long)norm, (unsigned long long)p, (unsigned long long)head);
                 ++bad;
             }
         }
     }
+    printf("shift-checked %ld\n", nsa);
     printf("checked %ld skipped %ld bad %ld\n", n, skipped, bad);
     return bad != 0;
 }
@@ -106,3 +122,5 @@ def test_renorm_word_matches_reference_loop(tmp_path):
     line = out.stdout.strip().splitlines()[-1]
     assert line.startswith("checked") and line.endswith("bad 0"), line
     assert int(line.split()[1]) > 2_000_000
+    nsa = int(out.stdout.strip().splitlines()[-2].split()[1])
+    assert nsa > 2_000_000, out.stdout
