@@ -423,7 +423,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             else sa_img[p] = static_cast<uint8_t>(sa);
         }
     }
-    if (ft.enc_wide) {
+    if (ft.enc_wide && pmax <= 0xFFFFu) {  // (pmf from two low halves: every mass below 2^16)
         const uint32_t budget = 4 * fast::kWideEncCumMax - (sa_img.empty() ? 0 : fast::kWideSaBytes);
         auto img_bytes = [](uint32_t nl) {
             const uint32_t ooff = 4 * ((nl >> 4) + 2);
@@ -441,10 +441,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             pack_img.assign(img_bytes(nlp) / 4, 0);
             for (uint32_t k = 0; k < (nlp >> 4) + 2; ++k) pack_img[k] = cum[std::min<uint32_t>(16 * k, nsym + 5)];
             auto* o16 = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(pack_img.data()) + ooff);
-            for (uint32_t k = 0; k < nlp + 2; ++k) {
-                const uint32_t sidx = std::min<uint32_t>(k, nsym + 5);
-                o16[k] = k < nlp ? static_cast<uint16_t>(cum[sidx] - cum[16 * (k >> 4)]) : 0;
-            }
+            for (uint32_t k = 0; k < nlp + 2; ++k) o16[k] = static_cast<uint16_t>(cum[std::min<uint32_t>(k, nsym + 5)]);
             ft.enc_pack = 1;
             ft.enc_nl = nlp;
             ft.enc_pack_ooff = ooff;

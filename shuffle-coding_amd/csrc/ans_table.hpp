@@ -109,9 +109,11 @@ struct FastTable {
     uint32_t dec_w_shp;
     uint32_t dec_w_nbp;
     uint32_t dec_w_cum_off;    // LDS offset of the cdf prefix from the s0 array (16-aligned)
-    // k_encode_w with a packed LDS prefix (enc_pack): cdf(s) = B[s >> 4] + O[s] for s < enc_nl,
-    // B (u32, enc_nl/16 + 2 entries) at the image's start and O (u16, enc_nl + 2 entries) at
-    // byte enc_pack_ooff: 2.25 B per symbol instead of 4, so a longer prefix fits
+    // k_encode_w with a packed LDS prefix (enc_pack): B[b] = cdf(16 b) (u32, enc_nl/16 + 2
+    // entries) at the image's start and O[s] = cdf(s) mod 2^16 (u16, enc_nl + 2 entries) at byte
+    // enc_pack_ooff, for tables whose masses are below 2^16 and whose blocks of 16 masses keep
+    // cdf(s) - B[s >> 4] below 2^16: cdf(s) = B + ((O[s] - B) mod 2^16), pmf(s) = (O[s+1] - O[s])
+    // mod 2^16.  2.25 B per symbol instead of 4, so a longer prefix fits
     const uint32_t* enc_pack_img;
     uint32_t enc_pack;
     uint32_t enc_pack_ooff;

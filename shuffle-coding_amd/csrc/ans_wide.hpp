@@ -69,9 +69,9 @@ __device__ __forceinline__ double rcp_newton(uint32_t p) {
 // Groups of 128 B of symbols (8 units of 16 B) per lane, walked last to first; each unit's rows
 // are requested at the point before it (LDS or global, per lane), so their latency hides behind
 // one unit of work.  Points and the byte funnel are ans_fast.hpp's.
-// kPack: the LDS prefix is the packed image (FastTable::enc_pack): a row costs a ds_read2_b32
-// of two block bases and two ds_read_u16 of offsets plus ~6 VALU, for ~1.8x the prefix (67%
-// of C4's symbols instead of 37%; the rest is the L2 request each).
+// kPack: the LDS prefix is the packed image (FastTable::enc_pack): a row costs a ds_read_b32 of
+// the block base and two ds_read_u16 of low halves plus 3 VALU (lrow), for ~1.8x the prefix
+// (64% of C4's symbols instead of 37%; the rest is the L2 request each).
 // kSa: every mass is at most kWideSaMax (FastTable::enc_sa) and its renorm shift sa(p) is one
 // LDS byte at address p: k = sa/8 - 1 + [head >= p*K << sa] (ans_renorm.hpp enc_sa), one 64-bit
 // shift and compare where the bit-length renorm takes three v_ffbh, two v_min, four adds, the
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     // a unit's rows: every lane reads the LDS pair of min(s, nl) (always in range) and the lanes
     // whose symbol lies past the prefix also load the global pair, into separate registers (a
     // shared destination would make each LDS read wait for every outstanding global load)
-    // (packed: lbuf holds the two block bases and the two offsets, combined in process)
+    // (packed: lbuf holds the block base and the two low halves, combined in process)
     using LRow = typename std::conditional<kPack, uint4, v2u32>::type;
     const uint32_t ooff = Lay::cum + t.enc_pack_ooff;
     auto request = [&](const uint4& unit, LRow* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
@@ -146,21 +146,33 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
             const uint32_t sp = umin(s, nl);
             if constexpr (kPack) {
-                const v2u32 b = cum_pair_lds(Lay::cum, sp >> 4);
+                const uint32_t b = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(Lay::cum + 4 * (sp >> 4)));
                 const uint32_t oa = ooff + 2 * sp;
-                lbuf[j] = make_uint4(b.x, b.y, *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa)),
-                                     *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa + 2)));
+                lbuf[j] = make_uint4(b, *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa)),
+                                     *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa + 2)), 0u);
             } else {
                 lbuf[j] = cum_pair_lds(Lay::cum, sp);
             }
             if (s >= nl) gbuf[j] = cum_pair_global(gcum, s);
         }
     };
-    auto lrow = [&](const LRow& r, uint32_t s) __attribute__((always_inline)) {
-        if constexpr (kPack) {  // cdf(s) = B[s >> 4] + O[s]; cdf(s + 1) from the next base at a block end
-            return v2u32{r.x + r.z, ((s + 1) & 15u) ? r.x + r.w : r.y};
+    // (cdf(s), pmf(s)) of a prefix symbol.  Packed (ans_kernels.hip build_fast_table): B = cdf(16 b)
+    // of its block and the low halves O(s) = cdf(s) mod 2^16, O(s + 1); within a block cdf(s) -
+    // B < 2^16 and every mass is below 2^16, so cdf(s) = B + ((O(s) - B) mod 2^16) and
+    // pmf(s) = (O(s + 1) - O(s)) mod 2^16: a u32 subtract, an SDWA add of its low half and a
+    // 16-bit subtract, with no select at block ends (offsets from each block's base needed the
+    // next block's base for s = 16 b + 15)
+    auto lrow = [&](const LRow& r) __attribute__((always_inline)) {
+        if constexpr (kPack) {
+            uint32_t cum, p;
+            const uint32_t d = r.y - r.x;
+            asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                : "=v"(cum) : "v"(r.x), "v"(d));
+            asm("v_sub_u16_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0"
+                : "=v"(p) : "v"(r.z), "v"(r.y));
+            return v2u32{cum, p};
         } else {
-            return r;
+            return v2u32{r.x, r.y - r.x};
         }
     };
     // renorm(p*K) (src/ans.rs:100,246-253): k = #{j >= 1 : (head >> 8j) >= p*K} bytes out
@@ -181,9 +193,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     // the row of symbol j of a unit: cdf(x), pmf(x) (src/codec.rs:63-64)
     auto row_of = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, int j) __attribute__((always_inline)) {
         const uint32_t sj = umin(sym_of<Sym>(unit, j), nsym);
-        const bool in_lds = sj < nl;
-        const v2u32 row = in_lds ? lrow(lbuf[j], sj) : gbuf[j];
-        return v2u32{row.x, row.y - row.x};
+        return sj < nl ? lrow(lbuf[j]) : v2u32{gbuf[j].x, gbuf[j].y - gbuf[j].x};
     };
     auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, uint32_t upos) __attribute__((always_inline)) {
         // kSa: the unit's rows and shift bytes first (p <= kWideSaMax: the byte at LDS address p)
@@ -201,7 +211,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
             const v2u32 row = kSa ? rows[j] : row_of(unit, lbuf, gbuf, j);
             const uint32_t cum = row.x, p = row.y;
-            asm volatile("v_min_u32 %0, %0, %1" : "+v"(minmass) : "v"(p));
             const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
             uint32_t k8;
             if constexpr (kSa) {
@@ -213,10 +222,25 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             f.push(lo32(head), k8);
             head >>= k8;
             // q = head / p, r = head % p (src/ans.rs:101-102), head = norm*q + cdf(x, r)
-            // (src/ans.rs:103-104): ans_fast.hpp push_one's form, with 1/p from rcp_newton
-            const uint64_t qb = qest_m1(head, rcp_newton(p));
-            const uint32_t rm = lo32(head) - lo32(qb) * p;
-            const uint32_t a = cum + rm + (rm >= p ? norm - p : 0u);
+            // (src/ans.rs:103-104): ans_fast.hpp push_one's form, with 1/p from rcp_newton.
+            // The estimate is rounded to nearest (qest_half) and the rare lanes where it is not q
+            // take the exact 64-bit remainder on a voted branch: rcp_newton is within 2^-47.9 of
+            // 1/p (v_rcp_f64 within 2^-24, squared by the Newton step, plus roundings) and
+            // head/p < 2^64 / norm <= 2^42, so the estimate is within 2^-5.9 of head/p (C4,
+            // norm 2^27: 2^-10.9, the branch in ~7% of wave steps) and q_est is q - 1, q or
+            // q + 1.  The estimate from below (qest_m1) needed a borrow-select on every push.
+            uint64_t qb = qest_half(head, rcp_newton(p));
+            uint32_t rm = lo32(head) - lo32(qb) * p;
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= p) != 0, 0)) {
+                if (rm >= p) {  // a zero-mass push (p = 0: rm >= 0 = p) always lands here
+                    minmass = min(minmass, p);
+                    const int64_t r = static_cast<int64_t>(head - (qb - 0x4330000000000000ull) * p);
+                    const int64_t d = r < 0 ? -1 : 1;
+                    qb += static_cast<uint64_t>(d);
+                    rm = static_cast<uint32_t>(r - d * static_cast<int64_t>(p));
+                }
+            }
+            const uint32_t a = cum + rm;
             const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * norm + a;
             uint32_t hq;
             asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb)), "s"(norm));
