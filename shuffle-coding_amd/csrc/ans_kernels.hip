@@ -424,13 +424,13 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         }
     }
     if (ft.enc_wide && pmax <= 0xFFFFu) {  // (pmf from two low halves: every mass below 2^16)
-        const uint32_t budget = 4 * fast::kWideEncCumMax - (sa_img.empty() ? 0 : fast::kWideSaBytes);
+        const uint32_t nl_max = fast::wide_pack_nl_max(!sa_img.empty());  // (the LDS regions, ans_wide.hpp)
         auto img_bytes = [](uint32_t nl) {
             const uint32_t ooff = 4 * ((nl >> 4) + 2);
             return (ooff + 2 * (nl + 2) + 3) & ~3u;
         };
         uint32_t nlp = 0;
-        while (nlp + 16 <= nsym && img_bytes(nlp + 16) <= budget) {
+        while (nlp + 16 <= nsym && nlp + 16 <= nl_max) {
             bool fits = true;
             for (uint32_t k = nlp; k < nlp + 16 && fits; ++k) fits = cum[k + 1] - cum[nlp] <= 0xFFFFu || ((k + 1) & 15) == 0;
             if (!fits) break;
@@ -450,6 +450,15 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         }
     }
     if (!ft.enc_sa) sa_img.clear();
+    // the packed encoder's global rows (ans_table.hpp enc_grow): (cdf(s), O(s) | O(s+1) << 16)
+    std::vector<uint32_t> grow;
+    if (ft.enc_pack) {
+        grow.resize(2 * (static_cast<size_t>(nsym) + 1));
+        for (uint32_t k = 0; k <= nsym; ++k) {
+            grow[2 * k] = cum[k];
+            grow[2 * k + 1] = (cum[k] & 0xFFFFu) | (cum[k + 1] << 16);
+        }
+    }
     // k_decode_w's LDS prefix: for each bucket width 2^shp, the longest prefix of symbols whose
     // bucket starts (u16) and cdf fit beside the ring; keep the width whose prefix covers the most
     // probability among those whose cf needs a fifth candidate at most 0.1% of the time
@@ -526,7 +535,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const size_t o_pack = o_decc + ((decc_b + 255) & ~size_t(255));
     const size_t pack_b = sizeof(uint32_t) * pack_img.size();
     const size_t o_sa = o_pack + ((pack_b + 255) & ~size_t(255));
-    const size_t o_uimg = o_sa + ((sa_img.size() + 255) & ~size_t(255));
+    const size_t o_grow = o_sa + ((sa_img.size() + 255) & ~size_t(255));
+    const size_t o_uimg = o_grow + ((4 * grow.size() + 255) & ~size_t(255));
     HIP_TRY(hipSetDevice(gt->g->device));
     void* mem = nullptr;
     HIP_TRY(hipMalloc(&mem, o_uimg + uimg.size() + 16));
@@ -551,6 +561,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.enc_pack_img = reinterpret_cast<const uint32_t*>(base + o_pack);
     if (!sa_img.empty()) HIP_TRY(hipMemcpy(base + o_sa, sa_img.data(), sa_img.size(), hipMemcpyHostToDevice));
     ft.enc_sa_img = reinterpret_cast<const uint32_t*>(base + o_sa);
+    if (!grow.empty()) HIP_TRY(hipMemcpy(base + o_grow, grow.data(), 4 * grow.size(), hipMemcpyHostToDevice));
+    ft.enc_grow = reinterpret_cast<const uint32_t*>(base + o_grow);
     if (!uimg.empty()) HIP_TRY(hipMemcpy(base + o_uimg, uimg.data(), uimg.size(), hipMemcpyHostToDevice));
     ft.dec_u_img = reinterpret_cast<const uint32_t*>(base + o_uimg);
     ft.dec_w_s0 = reinterpret_cast<const uint16_t*>(base + o_ws0);

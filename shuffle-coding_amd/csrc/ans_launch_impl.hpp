@@ -299,7 +299,8 @@ constexpr int kNotStaged = -2;
 
 // dynamic LDS of k_encode_w: the shift table (kSa), the ring and the prefix image
 inline size_t wide_enc_lds(const FastTable& ft) {
-    return (ft.enc_sa ? fast::kWideSaBytes : 0) + fast::kWideEncCum + (ft.enc_pack ? ft.enc_pack_bytes : 4 * (ft.enc_nl + 1));
+    if (!ft.enc_pack) return fast::kWideEncCum + 4 * (ft.enc_nl + 1);
+    return (ft.enc_sa ? fast::kWideSaBytes : 0) + fast::kWideBBytes + fast::kEncRingBytes + (ft.enc_pack_bytes - ft.enc_pack_ooff);
 }
 
 // The staged route applies to the large-alphabet fast kernels (u16 / u32 symbols).

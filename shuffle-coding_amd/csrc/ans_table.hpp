@@ -118,6 +118,9 @@ struct FastTable {
     uint32_t enc_pack;
     uint32_t enc_pack_ooff;
     uint32_t enc_pack_bytes;  // image bytes (a multiple of 4), staged into LDS as u32 words
+    // ... and its global rows for s >= enc_nl in the LDS rows' form (B, O(s) | O(s+1) << 16):
+    // (cdf(s), cdf(s) mod 2^16 | cdf(s+1) << 16), 8 B per symbol 0..nsym, one load each
+    const uint32_t* enc_grow;
     // k_encode_w<kSa> (every mass <= fast::kWideSaMax, with the packed prefix): the renorm shift
     // of each mass, sa(p) = 8 (k0(p) + 1) with T = p*K << sa(p) (ans_renorm.hpp enc_sa), one
     // byte per mass at LDS offset 0 (fast::kWideSaBytes, staged from enc_sa_img)

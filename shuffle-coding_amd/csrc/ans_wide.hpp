@@ -24,9 +24,10 @@
 namespace shuffle_coding {
 namespace fast {
 
-// ---- encoder LDS: the byte ring at offset 0 (64 KiB, 512 lanes), the cdf prefix after it.
-// kSa kernels put the per-mass renorm shifts first (kWideSaBytes at offset 0, so a shift's
-// address is the mass itself) and the ring and the prefix kWideSaBytes higher.
+// ---- encoder LDS.  Plain prefix: the byte ring at offset 0 (64 KiB, 512 lanes), the cdf
+// prefix after it.  Packed prefix: the per-mass renorm shifts first when kSa (kWideSaBytes at
+// offset 0, so a shift's address is the mass itself), the block bases (kWideBBytes, below 64 KiB
+// so their base folds into the ds offset field), the ring, then the low halves.
 constexpr uint32_t kWideRing = 0;
 constexpr uint32_t kWideEncCum = kEncRingBytes;
 constexpr uint32_t kWideEncCumMax = (160u * 1024u - kWideEncCum) / 4u;  // staged cdf entries
@@ -34,13 +35,22 @@ constexpr uint32_t kWideNormMin = 1u << 22;  // one Newton step suffices above (
 constexpr uint32_t kWideSaMax = 4096;        // largest mass with a shift byte (12-bit masses)
 constexpr uint32_t kWideSaBytes = 4352;      // (kWideSaMax + 1) bytes, rounded up to 256
 static_assert(kWideSaBytes >= kWideSaMax + 1 && kWideSaBytes % 256 == 0, "shift table");
-template <bool kSa>
+constexpr uint32_t kWideBBytes = 10752;      // packed block bases: up to 2,688 (43,000 symbols)
+template <bool kSa, bool kPack>
 struct WideEncLds {
-    static constexpr uint32_t ring = kSa ? kWideSaBytes : kWideRing;
-    static constexpr uint32_t cum = ring + kEncRingBytes;  // the prefix image
+    static constexpr uint32_t b = kSa ? kWideSaBytes : 0;               // packed: block bases
+    static constexpr uint32_t ring = kPack ? b + kWideBBytes : kWideRing;
+    static constexpr uint32_t cum = ring + kEncRingBytes;               // plain cdf / packed low halves
 };
+// the packed prefix's capacity: nl symbols need (nl/16 + 2) bases and nl + 2 low halves
+constexpr uint32_t wide_pack_nl_max(bool sa) {
+    const uint32_t o_bytes = 160u * 1024u - ((sa ? kWideSaBytes : 0) + kWideBBytes + kEncRingBytes);
+    const uint32_t by_o = (o_bytes / 4u) * 2u - 2u, by_b = ((kWideBBytes / 4u) - 2u) * 16u;
+    return (by_o < by_b ? by_o : by_b) & ~15u;
+}
 
 typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 // (cdf(s), cdf(s+1)) from the global cdf array: one 8-B load at a 4-B aligned address
@@ -87,12 +97,17 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
                                                          uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
                                                          ChunkInit ini, const uint32_t* __restrict__ vlen = nullptr) {
     static_assert(!kSa || kPack, "the shift table comes with the packed prefix");
-    using Lay = WideEncLds<kSa>;
+    using Lay = WideEncLds<kSa, kPack>;
     extern __shared__ __align__(16) unsigned char lds[];
     {
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + Lay::cum);
-        if constexpr (kPack) {
-            for (uint32_t i = threadIdx.x; i < t.enc_pack_bytes / 4; i += kBlock) lc[i] = t.enc_pack_img[i];
+        if constexpr (kPack) {  // the image's bases and low halves to their two regions
+            uint32_t* lb = reinterpret_cast<uint32_t*>(lds + Lay::b);
+            const uint32_t nb = t.enc_pack_ooff / 4;
+            for (uint32_t i = threadIdx.x; i < t.enc_pack_bytes / 4; i += kBlock) {
+                if (i < nb) lb[i] = t.enc_pack_img[i];
+                else lc[i - nb] = t.enc_pack_img[i];
+            }
         } else {
             for (uint32_t i = threadIdx.x; i <= t.enc_nl; i += kBlock) lc[i] = t.cum[i];
         }
@@ -137,39 +152,54 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     // a unit's rows: every lane reads the LDS pair of min(s, nl) (always in range) and the lanes
     // whose symbol lies past the prefix also load the global pair, into separate registers (a
     // shared destination would make each LDS read wait for every outstanding global load)
-    // (packed: lbuf holds the block base and the two low halves, combined in process)
-    using LRow = typename std::conditional<kPack, uint4, v2u32>::type;
-    const uint32_t ooff = Lay::cum + t.enc_pack_ooff;
-    auto request = [&](const uint4& unit, LRow* lbuf, v2u32* gbuf) __attribute__((always_inline)) {
+    // A unit's rows land in ONE pair of registers per symbol whichever part of the table holds
+    // them: every lane reads the LDS prefix at min(s, nl), then the lanes with s >= nl overwrite
+    // those registers from global memory with a row that the same combination (lrow) turns into
+    // (cdf(s), pmf(s)), so process selects nothing (packed: FastTable::enc_grow; plain: (cdf(s),
+    // cdf(s+1))).  The global loads follow all of the unit's LDS reads: the compiler orders a
+    // load after a pending LDS write to the same registers with an lgkmcnt wait, once per unit
+    // where interleaving them would wait once per symbol.  (Separate registers took a select,
+    // which the compiler made an exec-masked branch per symbol: six SALU and a v_mov.)
+    // Packed rows: (B, O(s) | O(s+1) << 16), the two low halves in one register (lrow reads
+    // them by halves; as separate u32 values each took a v_and).
+    using LRow = v2u32;
+    auto request = [&](const uint4& unit, LRow* lbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
-            const uint32_t sp = umin(s, nl);
+            const uint32_t sp = umin(umin(sym_of<Sym>(unit, j), nsym), nl);
             if constexpr (kPack) {
-                const uint32_t b = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(Lay::cum + 4 * (sp >> 4)));
-                const uint32_t oa = ooff + 2 * sp;
-                lbuf[j] = make_uint4(b, *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa)),
-                                     *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa + 2)), 0u);
+                const uint32_t b = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(Lay::b + 4 * (sp >> 4)));
+                uint32_t oa;  // Lay::cum + 2 sp in one v_lshl_add (the base lies past the 16-bit ds
+                              // offsets; from C++ the compiler formed oa and oa + 2 with two v_add)
+                asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(oa) : "v"(sp), "s"(Lay::cum));
+                us2 o;
+                o.x = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa));
+                o.y = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(oa + 2));
+                lbuf[j] = v2u32{b, __builtin_bit_cast(uint32_t, o)};
             } else {
                 lbuf[j] = cum_pair_lds(Lay::cum, sp);
             }
-            if (s >= nl) gbuf[j] = cum_pair_global(gcum, s);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
+            if (s >= nl) lbuf[j] = kPack ? cum_pair_global(t.enc_grow, 2 * s) : cum_pair_global(gcum, s);
         }
     };
-    // (cdf(s), pmf(s)) of a prefix symbol.  Packed (ans_kernels.hip build_fast_table): B = cdf(16 b)
-    // of its block and the low halves O(s) = cdf(s) mod 2^16, O(s + 1); within a block cdf(s) -
-    // B < 2^16 and every mass is below 2^16, so cdf(s) = B + ((O(s) - B) mod 2^16) and
-    // pmf(s) = (O(s + 1) - O(s)) mod 2^16: a u32 subtract, an SDWA add of its low half and a
-    // 16-bit subtract, with no select at block ends (offsets from each block's base needed the
-    // next block's base for s = 16 b + 15)
+    // (cdf(s), pmf(s)) of a symbol.  Packed (ans_kernels.hip build_fast_table): B = cdf(16 b) of
+    // its block and the low halves O(s) = cdf(s) mod 2^16, O(s + 1); within a block cdf(s) - B
+    // < 2^16 and every mass is below 2^16, so cdf(s) = B + ((O(s) - B) mod 2^16) and pmf(s) =
+    // (O(s + 1) - O(s)) mod 2^16: a 16-bit subtract, an SDWA add of its low half and a 16-bit
+    // subtract, with no select at block ends (offsets from each block's base needed the next
+    // block's base for s = 16 b + 15).  A global row (B = cdf(s)) gives the same.
     auto lrow = [&](const LRow& r) __attribute__((always_inline)) {
         if constexpr (kPack) {
-            uint32_t cum, p;
-            const uint32_t d = r.y - r.x;
+            uint32_t d, cum, p;  // (d: only its low half is defined and read)
+            asm("v_sub_u16 %0, %1, %2" : "=v"(d) : "v"(r.y), "v"(r.x));
             asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
                 : "=v"(cum) : "v"(r.x), "v"(d));
-            asm("v_sub_u16_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0"
-                : "=v"(p) : "v"(r.z), "v"(r.y));
+            asm("v_sub_u16_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0"
+                : "=v"(p) : "v"(r.y), "v"(r.y));
             return v2u32{cum, p};
         } else {
             return v2u32{r.x, r.y - r.x};
@@ -191,25 +221,21 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         return (head >> m8) >= pK ? m8 : m8 - 8u;
     };
     // the row of symbol j of a unit: cdf(x), pmf(x) (src/codec.rs:63-64)
-    auto row_of = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, int j) __attribute__((always_inline)) {
-        const uint32_t sj = umin(sym_of<Sym>(unit, j), nsym);
-        return sj < nl ? lrow(lbuf[j]) : v2u32{gbuf[j].x, gbuf[j].y - gbuf[j].x};
-    };
-    auto process = [&](const uint4& unit, const LRow* lbuf, const v2u32* gbuf, uint32_t upos) __attribute__((always_inline)) {
+    auto process = [&](const LRow* lbuf, uint32_t upos) __attribute__((always_inline)) {
         // kSa: the unit's rows and shift bytes first (p <= kWideSaMax: the byte at LDS address p)
         v2u32 rows[U];
         uint32_t sas[U];
         if constexpr (kSa) {
 #pragma unroll
             for (int j = U - 1; j >= 0; --j) {
-                rows[j] = row_of(unit, lbuf, gbuf, j);
+                rows[j] = lrow(lbuf[j]);
                 sas[j] = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(rows[j].y));
             }
         }
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
-            const v2u32 row = kSa ? rows[j] : row_of(unit, lbuf, gbuf, j);
+            const v2u32 row = kSa ? rows[j] : lrow(lbuf[j]);
             const uint32_t cum = row.x, p = row.y;
             const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
             uint32_t k8;
@@ -257,9 +283,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
     }
     LRow la[U], lb[U];
-    v2u32 ga[U], gb[U];
     wait_vm();
-    request(n[GU - 1], la, ga);
+    request(n[GU - 1], la);
     for (int g = ngroups - 1; g >= 0; --g) {
         uint4 cc[GU];
 #pragma unroll
@@ -272,14 +297,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             else wait_vm();
             flush();
             const bool odd = (u & 1) != 0;
-            if (u > 0) request(cc[u - 1], odd ? lb : la, odd ? gb : ga);
+            if (u > 0) request(cc[u - 1], odd ? lb : la);
             if (u == GU - 1 && g > 0) {
                 const uint4* gsrc = src + GU * (g - 1);
 #pragma unroll
                 for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
             }
-            if (u == 0) request(n[GU - 1], la, ga);  // unit GU-1 of group g-1 (landed units ago)
-            process(cc[u], odd ? la : lb, odd ? ga : gb, static_cast<uint32_t>(g * GS + u * U));
+            if (u == 0) request(n[GU - 1], la);  // unit GU-1 of group g-1 (landed units ago)
+            process(odd ? la : lb, static_cast<uint32_t>(g * GS + u * U));
         }
     }
     wait_vm();
