@@ -48,6 +48,10 @@ constexpr uint32_t wide_pack_nl_max(bool sa) {
     const uint32_t by_o = (o_bytes / 4u) * 2u - 2u, by_b = ((kWideBBytes / 4u) - 2u) * 16u;
     return (by_o < by_b ? by_o : by_b) & ~15u;
 }
+static_assert(WideEncLds<true, true>::cum + ((2u * (wide_pack_nl_max(true) + 2u) + 3u) & ~3u) <= 160u * 1024u &&
+                  WideEncLds<false, true>::cum + ((2u * (wide_pack_nl_max(false) + 2u) + 3u) & ~3u) <= 160u * 1024u &&
+                  4u * ((wide_pack_nl_max(false) >> 4) + 2u) <= kWideBBytes && WideEncLds<true, true>::ring <= 65535u,
+              "packed prefix regions fit one CU's LDS (the ring base in the 16-bit ds offsets)");
 
 typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
