@@ -387,7 +387,7 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
           if constexpr (sizeof(Sym) > 1) {
             const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
             if (ft.dec_c)
-                fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+                fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
             else
                 fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
           }
@@ -538,9 +538,9 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
                 // leaves room for two workgroups per CU when a shard has the chunks for them
                 if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0) {
                     if (ft.pmax < (1u << 24))
-                        fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                        fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                     else
-                        fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, fast::kWideDecTab, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                        fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                 }
                 else if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
                     fast::k_decode_w<Sym, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);

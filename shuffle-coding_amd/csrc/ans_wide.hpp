@@ -356,6 +356,7 @@ static_assert((1u << kWideDecRowShift) == kWideDecLanes * 4, "row bytes");
 constexpr uint32_t kWideDecTab = kWideDecRows * kWideDecLanes * 4;  // 67,584 B of ring, then the tables
 static_assert(kWideDecTab % 256 == 0, "table base");
 constexpr uint32_t kWideDecTabBytes = 160u * 1024u - kWideDecTab;
+constexpr uint32_t kWideDecBktLds = kWideDecTabBytes / 16;  // compact buckets staged beside the ring
 __device__ const uint4 kZeroPair[8] = {};  // 128 zero bytes: pages below the stream start
 
 struct DecChainW {
@@ -526,6 +527,22 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideDecTab + t.dec_w_cum_off);
         for (uint32_t i = threadIdx.x; i <= t.dec_w_nlp + 5; i += kWideDecLanes) lc[i] = t.cum[i];
     }
+    // compact buckets without the prefix (C4): the first nlb buckets are staged in the LDS the
+    // ring leaves (kWideDecBktLds: 6,016 of C4's 65,704), so that share of the lookups issues no
+    // L2 request (the decoder runs at ~0.87 of the L2 gather ceiling)
+    const uint32_t nlb = [&]() -> uint32_t {
+        if constexpr (kCompact && !kPrefix) {
+            const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> t.dec_c_shift) + 1);
+            return umin(nb, kWideDecBktLds);
+        } else {
+            return 0;
+        }
+    }();
+    if constexpr (kCompact && !kPrefix) {
+        const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt_c);
+        uint4* lb = reinterpret_cast<uint4*>(lds + kWideDecTab);
+        for (uint32_t i = threadIdx.x; i < nlb; i += kWideDecLanes) lb[i] = gb[i];
+    }
     __syncthreads();
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kWideDecLanes + threadIdx.x;
     if (c >= nfull) return;  // no barrier below: lanes are independent
@@ -563,7 +580,15 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
         // global bucket (lanes past the prefix only): issued first, the longer round trip
         uint4 ga = make_uint4(0, 0, 0, 0), gb = make_uint4(0, 0, 0, 0);
         if (!pre) {
-            if constexpr (kCompact) {
+            if constexpr (kCompact && !kPrefix) {  // the LDS copy of the first nlb buckets, else L2
+                const uint32_t bi = cf >> cshift;
+                uint4 g = make_uint4(0, 0, 0, 0);
+                if (bi >= nlb) g = *reinterpret_cast<const uint4*>(bktc + bi);  // c0 | s0, d0 | d1, d2 | d3, d4
+                uint32_t la;
+                asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(la) : "v"(umin(bi, nlb - 1)), "s"(kWideDecTab));
+                const uint4 l = lds_ld128(la);
+                ga = bi < nlb ? l : g;
+            } else if constexpr (kCompact) {
                 ga = *reinterpret_cast<const uint4*>(bktc + (cf >> cshift));  // c0 | s0, d0 | d1, d2 | d3, d4
             } else {
                 const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
