@@ -361,15 +361,28 @@ def c4_pass(ctx, args):
     return [elapsed, enc_ms, dec_ms, comp, bad], names, n, int(masses.sum())
 
 
+def c4_l2_share(norm):
+    """The share of k_decode_w's bucket lookups that go to L2: its compact buckets have the finest
+    width with at most 2^17 of them (ans_kernels.hip build_fast_table), and the first
+    kWideDecBktLds = (160 KiB - 67,584 B of ring) / 16 = 6,016 are read from LDS (ans_wide.hpp);
+    cf is uniform over the buckets."""
+    cs = 0
+    while ((norm - 1) >> cs) + 1 > (1 << 17):
+        cs += 1
+    nb = ((norm - 1) >> cs) + 1
+    return 1.0 - min(nb, (160 * 1024 - 67584) // 16) / nb
+
+
 def c4_summary(rows, names, n, norm, args, world):
     """The c4 sub-object from every rank's [elapsed, enc_ms, dec_ms, comp, bad]."""
     sym_bytes = 2
     wall = max(r[0] for r in rows)
+    share = c4_l2_share(norm)
     per = []
     for r in rows:
         alg = n * sym_bytes + r[3]
         per.append({"encode_ms": r[1], "decode_ms": r[2], "dec_frac": alg / (r[2] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "enc_frac": alg / (r[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, "req_s": n / (r[2] * 1e-3)})
+                    "enc_frac": alg / (r[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, "req_s": n * share / (r[2] * 1e-3)})
     ceil, ceil_src = l2_ceiling()
     r0 = per[0]
     out = {
@@ -385,7 +398,9 @@ def c4_summary(rows, names, n, norm, args, world):
         "compressed_bytes_per_symbol": round(rows[0][3] / n, 5),
         "kernels": {"encode": names[0], "decode": names[1]},
         "roofline": {
-            "bound": "l2-requests (decode: one random 16-B bucket gather per symbol on the chain)",
+            "bound": "l2-requests (decode: one random 16-B bucket gather per symbol on the chain, "
+                     "past the buckets staged in LDS)",
+            "decode_l2_share_of_lookups": round(share, 4),
             "decode_hbm_frac": round(r0["dec_frac"], 4),
             "encode_hbm_frac": round(r0["enc_frac"], 4),
             "decode_l2_req_per_s": round(r0["req_s"]),
