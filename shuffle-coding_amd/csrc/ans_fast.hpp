@@ -1084,8 +1084,14 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                     __builtin_amdgcn_sched_barrier(0);
                     if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
                     if constexpr (kMode == kModeU) {
+                        // The chain's dependent part up to the bucket read at raised wave priority:
+                        // the arbiter then issues it ahead of the other waves' symbol bookkeeping,
+                        // so the LDS round trip starts sooner (decode -6% in a same-box A/B,
+                        // DESIGN.md §3.1)
+                        __builtin_amdgcn_s_setprio(2);
                         ch.template renorm_div_u<kJ4>(L, hL8, norm, rcp_norm, magic_m1);
                         ch.lookup_u(shift, 32u - shift);
+                        __builtin_amdgcn_s_setprio(0);
                     } else {
                         ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
                         if constexpr (kFar) {
