@@ -239,6 +239,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
 #pragma unroll
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
+            __builtin_amdgcn_s_setprio(2);  // the push at raised wave priority (encode -0.4%, A/B)
             const v2u32 row = kSa ? rows[j] : lrow(lbuf[j]);
             const uint32_t cum = row.x, p = row.y;
             const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             uint32_t hq;
             asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb)), "s"(norm));
             head = mk64(hi32(lo64) + hq - exp_norm, lo32(lo64));
+            __builtin_amdgcn_s_setprio(0);
         }
     };
 
@@ -574,6 +576,9 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
 
     auto step = [&]() __attribute__((always_inline)) {
+        // the chain's part up to the bucket loads at raised wave priority (ans_fast.hpp k_decode;
+        // decode -1.4% in a same-box A/B)
+        __builtin_amdgcn_s_setprio(2);
         ch.renorm_div(L, hL8, norm, rcp_norm);
         const uint32_t cf = ch.cf;
         const bool pre = kPrefix && cf < cpre;
@@ -596,6 +601,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
                 gb = e[1];  // c0..c3 | c4, c5, s0, -
             }
         }
+        __builtin_amdgcn_s_setprio(0);
         // LDS prefix (every lane; the bucket index clamped into the prefix)
         const uint32_t bi = umin(cf, cpre - 1) >> shp;
         const uint32_t s0 = *reinterpret_cast<const lds_u16*>(static_cast<uintptr_t>(kWideDecTab + 2 * bi));
