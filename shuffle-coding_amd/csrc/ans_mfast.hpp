@@ -733,6 +733,10 @@ struct IndepModel {
         const uint64_t L = mk64(h0.w, h0.z);
         const uint32_t norm = h1.x, hL8 = h1.y, bkt = h1.z;
         const uint32_t us = h1.w & 0xFFu, rsh = (h1.w >> 8) & 0xFFu, rows = h1.w >> 16;  // rows: 8 * 257 t
+        // the chain from the renorm to the bucket read at raised wave priority, as in the C3
+        // decoder (ans_fast.hpp k_decode): decode -1.3% (profiles/r04h_ab_rejected.txt; a second
+        // bracket around the row read gained nothing)
+        __builtin_amdgcn_s_setprio(2);
         ch.form_window();
         ch.P8 -= ch.renorm_up8(L, hL8);
         ch.read_window();  // for the next pop
@@ -741,6 +745,7 @@ struct IndepModel {
         uint32_t cf;
         fast::div_norm(ch.head, norm, rcp_norm, qq, cf);
         const uint64_t cc = lds_ld64(bkt + ((cf >> us) << 3));
+        __builtin_amdgcn_s_setprio(0);
         const uint32_t rx = cf << rsh;
         uint32_t sx;
         asm volatile(
