@@ -50,6 +50,8 @@ CONFIGS = {
     # name: (masses fn name, log2 n per rank, symbol bytes, seed)
     "c3": ("c3_masses", 30, 1, 1),
     "c3p2": ("c3_pow2_masses", 30, 1, 1),  # C3's table quantised to norm 2^24
+    "c3s": ("c3_small_masses", 30, 1, 1),  # ... to norm 32,749 (< 2^16: count-built dataset tables)
+    "c3b": ("c3_big_masses", 30, 1, 1),  # ... to norm 2^32 - 5 (> 2^31)
     "c4": ("c4_masses", 29, 2, 2),
 }
 
@@ -586,7 +588,7 @@ def main():
         c4 = c4_summary([r[6:] for r in rows], c4_names, c4_n, c4_norm, args, world)
 
     host = None
-    if world == 1 and not args.no_host and args.config in ("c3", "c3p2"):
+    if world == 1 and not args.no_host and args.config in ("c3", "c3p2", "c3s", "c3b"):
         host = host_pass(ctx, gt, syms, n, L)
         if not host.pop("ok"):
             raise SystemExit("host-memory round trip failed")

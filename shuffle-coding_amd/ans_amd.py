@@ -1150,11 +1150,9 @@ def c3_masses():
     return (np.uint64(1) + (splitmix64_np(np.uint64(0x5EED) ^ s) & np.uint64((1 << 20) - 1))).astype(np.uint64)
 
 
-def c3_pow2_masses():
-    """C3's table quantised to norm 2^24 (SURVEY.md §8d secondary C3): largest-remainder
-    rounding of c3_masses() * 2^24 / norm, every mass at least 1."""
-    m = c3_masses().astype(np.float64)
-    target = 1 << 24
+def quantise_masses(m, target):
+    """Largest-remainder rounding of masses m to sum exactly `target`, every mass at least 1."""
+    m = np.asarray(m, dtype=np.float64)
     exact = m * target / m.sum()
     q = np.maximum(1, np.floor(exact)).astype(np.int64)
     rem = target - int(q.sum())
@@ -1170,6 +1168,22 @@ def c3_pow2_masses():
             rem += 1
         i += 1
     return q.astype(np.uint64)
+
+
+def c3_pow2_masses():
+    """C3's table quantised to norm 2^24 (SURVEY.md §8d secondary C3)."""
+    return quantise_masses(c3_masses(), 1 << 24)
+
+
+def c3_small_masses():
+    """C3's table quantised to norm 32,749 (a prime below 2^15): the norm range of the
+    reference's dataset-level tables built from counts (src/benchmark.rs:552-578)."""
+    return quantise_masses(c3_masses(), 32749)
+
+
+def c3_big_masses():
+    """C3's table quantised to norm 4,294,967,291 (the largest prime below 2^32)."""
+    return quantise_masses(c3_masses(), 4294967291)
 
 
 def c4_masses():

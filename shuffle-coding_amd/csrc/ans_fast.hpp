@@ -83,6 +83,17 @@ constexpr int kModeFar = 0;   // 16-B buckets, three candidates, voted scan of t
 constexpr int kModeRows = 1;  // 8-B buckets, two boundaries, then the symbol's (cdf, pmf) row
 constexpr int kModeU = 2;     // kModeRows over u in [0, 2 norm): no quotient fix-up
 constexpr uint64_t kMaxMinHead = 1ull << 56;
+// norm ranges of the LDS-table kernels (k_encode / k_decode kNR; FastTable::nr):
+//  kNormStd    2^16 <= norm <= 2^31: head / d < 2^48, one f64 estimate within one of the quotient
+//  kNormSmall  norm < 2^16 (the reference's count-built dataset tables, src/benchmark.rs:552-578):
+//              head / d reaches 2^64 / norm, so the quotient is a long division in two f64
+//              estimates: qh = floor(H / d) - 1 exactly (H = hi32(head), from a reciprocal rounded
+//              UP, truncated), then the low part of x' = (H - qh d) 2^32 + lo32(head) < 2 d 2^32
+//  kNormBig    2^31 < norm < 2^32: the estimate is accurate (head / d < 2^33) but 32-bit
+//              remainders over [0, 2 norm) wrap, so the remainder is checked in 64 bits
+constexpr int kNormStd = 0;
+constexpr int kNormSmall = 1;
+constexpr int kNormBig = 2;
 
 // Non-temporal 16-byte global load / store (streamed data that must not evict cached tables).
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
@@ -161,6 +172,25 @@ __device__ __forceinline__ uint64_t qest_half(uint64_t x, double rcp) {
     double t;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "v"(xd), "v"(rcp), "v"(4503599627370495.5));
     return static_cast<uint64_t>(__double_as_longlong(t));
+}
+
+// v_cvt_u32_f64: truncates toward zero, negatives saturate to 0 (a C++ cast of a negative
+// double to an unsigned type is undefined)
+__device__ __forceinline__ uint32_t cvt_u32(double x) {
+    uint32_t r;
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// kNormSmall's first division step: with rcp_up >= 1/d rounded UP (by less than
+// 2^-52 relative; the host's rcp_up) and d < 2^16, trunc(fma(H, rcp_up, -1)) = floor(H / d) - 1
+// for every H < 2^32: the product overshoots H / d by less than 2^-19 < 1/d - the largest
+// fraction below 1 that H / d can have, and Q - 1 is representable (rounding is monotone).
+// Returns qh and replaces hd (= H as f64) by rh = H - qh d in [d, 2d), exactly.
+__device__ __forceinline__ uint32_t div_hi(double& hd, double rcp_up, double neg_d) {
+    const double qhf = __builtin_trunc(__builtin_fma(hd, rcp_up, -1.0));
+    hd = __builtin_fma(qhf, neg_d, hd);
+    return cvt_u32(qhf);
 }
 
 // TailGenerator::Random (src/ans.rs:129-164): rand_pcg 0.3.1 Pcg64Mcg (MCG-128, XSL-RR-64
@@ -356,7 +386,8 @@ struct PageOut {
 // kVar (LDS rows only): chunk c holds vlen[c] <= chunk_len symbols at the start of its stride
 // (staged ragged / variable-length chunks, ans_kernels.hip launch_staged_encode); the pushes
 // past vlen[c], all in its first-coded group, are skipped.
-template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kVar = false>
+// kNR: the norm range (kNormStd / kNormSmall / kNormBig above; LDS rows only for the latter two).
+template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kVar = false, int kNR = kNormStd>
 __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTable t, const Sym* __restrict__ syms,
                                                                          uint64_t chunk_len, uint64_t nfull,
                                                                          uint8_t* __restrict__ slots, uint64_t slot_cap,
@@ -364,6 +395,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                                                                          uint32_t* __restrict__ status, ChunkInit ini,
                                                                          const uint32_t* __restrict__ vlen = nullptr) {
     static_assert(!(kVar && kGlobalRows), "staged chunks take the LDS-row kernel");
+    static_assert(kNR == kNormStd || !kGlobalRows, "other norm ranges: LDS rows only");
     extern __shared__ __align__(16) unsigned char lds[];
     // a symbol's row is two random LDS reads: rcp by ds_read_b64 (32-lane groups over 32 bank
     // pairs) and {mass, cum, renorm word} by one ds_read_b128 (16-lane groups over 16 bank
@@ -453,13 +485,33 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         // and the rare lanes where it is not take the exact 64-bit remainder on a voted branch
         // (q_est = q - 1 or q + 1).  The common path is one compare and one add, where the
         // estimate from below (q_m in {q - 1, q}) needed a borrow-select on every symbol.
-        uint64_t qb = qest_half(head, e.rcp);  // q_est + 0x43300000'00000000
+        // kNormSmall: the same estimate on x' = (H - qh p) 2^32 + lo32(head) in [p 2^32, 2p 2^32)
+        // after the exact high step (div_hi; e.rcp is 1/p rounded up there), q = qh 2^32 + q_est
+        uint32_t qh = 0;
+        uint64_t qb;  // q_est + 0x43300000'00000000
+        if constexpr (kNR == kNormSmall) {
+            double hd;
+            asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
+            qh = div_hi(hd, e.rcp, -static_cast<double>(e.mass));
+            const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
+            double t;
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "v"(xd), "v"(e.rcp), "v"(4503599627370495.5));
+            qb = static_cast<uint64_t>(__double_as_longlong(t));
+        } else {
+            qb = qest_half(head, e.rcp);
+        }
         uint32_t rm = lo32(head) - lo32(qb) * e.mass;
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= e.mass) != 0, 0)) {
-            if (rm >= e.mass) {
+        // kNormBig: the 32-bit test cannot tell a remainder off by one estimate step from a true
+        // one for masses above 2^31 (2^32 - p < p), so those rows always take the exact branch
+        const bool fix = kNR == kNormBig ? (rm >= e.mass || static_cast<int32_t>(e.mass) < 0) : rm >= e.mass;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(fix) != 0, 0)) {
+            if (fix) {
                 minmass = min(minmass, e.mass);
-                const int64_t r = static_cast<int64_t>(head - (qb - 0x4330000000000000ull) * e.mass);
-                const int64_t d = r < 0 ? -1 : 1;
+                const uint64_t x = kNR == kNormSmall ? mk64(hi32(head) - qh * e.mass, lo32(head)) : head;
+                const int64_t r = static_cast<int64_t>(x - (qb - 0x4330000000000000ull) * e.mass);
+                // q_est is within one of q; off by one wherever the 32-bit test fired, except
+                // on kNormBig's forced rows, which may be right already
+                const int64_t d = r < 0 ? -1 : (kNR != kNormBig || r >= static_cast<int64_t>(e.mass) ? 1 : 0);
                 qb += static_cast<uint64_t>(d);
                 rm = static_cast<uint32_t>(r - d * static_cast<int64_t>(e.mass));
             }
@@ -469,7 +521,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         // comes off as a scalar): a second v_mad_u64_u32 costs two v_mov and the exponent a v_add
         const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * static_cast<uint32_t>(norm) + a;
         uint32_t hq;
-        asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb)), "s"(static_cast<uint32_t>(norm)));
+        asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hq) : "v"(hi32(qb) + qh), "s"(static_cast<uint32_t>(norm)));
         head = mk64(hi32(lo64) + hq - exp_norm, lo32(lo64));
     };
     const uint32_t nvalid = kVar ? vlen[c] : static_cast<uint32_t>(chunk_len);
@@ -665,16 +717,44 @@ __host__ __device__ inline uint32_t renorm_screen(uint64_t L) {
 // The estimate's raw f64 bits are q' + 0x43300000'00000000; q = q' - [ii < 0] and the exponent
 // come off in ONE 64-bit add of (m - 0x43300000 : m), m = ii >> 31 (0 or -1), where the compiler
 // emitted the sign extension, the 64-bit add and a separate v_add for the exponent word.
-__device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rcp_norm, uint64_t& qq, uint32_t& cf) {
+// kNormSmall: rcp_norm is 1/norm rounded up; the estimate divides x' = (H - qh norm) 2^32 + lo
+// after the exact high step (div_hi), and qh joins the high word of the same add.
+// kNormBig: 2^31 < norm, so ii does not fit 32 signed bits: the estimate is rounded to nearest
+// (within one of q: head / norm < 2^33), the remainder taken in 64 bits and, on the rare lanes
+// outside [0, norm), fixed on a voted branch.
+template <int kNR = kNormStd>
+__device__ __forceinline__ void div_norm(uint64_t head, uint32_t norm, double rcp_norm, uint64_t& qq, uint32_t& cf,
+                                         double neg_norm = 0.0) {
     double hd;
     asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
+    uint32_t qh = 0;
+    if constexpr (kNR == kNormSmall) qh = div_hi(hd, rcp_norm, neg_norm);
     const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
+    if constexpr (kNR == kNormBig) {
+        const double t = __builtin_fma(xd, rcp_norm, 4503599627370495.5);
+        const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(t));
+        qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));  // q_est < 2^33
+        uint64_t r = head - qq * norm;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(r >= norm) != 0, 0)) {
+            if (r >= norm) {
+                if (static_cast<int64_t>(r) < 0) {
+                    qq -= 1;
+                    r += norm;
+                } else {
+                    qq += 1;
+                    r -= norm;
+                }
+            }
+        }
+        cf = lo32(r);
+        return;
+    }
     const double t = __builtin_fma(xd, rcp_norm, 4503599627370496.0);
     const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(t));
     const int32_t ii = static_cast<int32_t>(lo32(head) - lo32(raw) * norm);
     const uint32_t m = static_cast<uint32_t>(ii >> 31);
     cf = static_cast<uint32_t>(ii) + (norm & m);
-    const uint64_t adj = mk64(m + 0xBCD00000u, m);  // -0x43300000'00000000 - [ii < 0]
+    const uint64_t adj = mk64(m + 0xBCD00000u + qh, m);  // -0x43300000'00000000 - [ii < 0] (+ qh 2^32)
     asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(qq) : "v"(raw), "v"(adj));
 }
 
@@ -872,18 +952,23 @@ struct DecChain {
         }
     }
     // phase 1: renorm_up, q/cf, next window
-    template <bool kJ4>
-    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
+    template <bool kJ4, int kNR = kNormStd>
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm,
+                                               double neg_norm = 0.0) {
         form_window();
         P8 -= static_cast<int32_t>(renorm_up8<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        div_norm(head, norm, rcp_norm, qq, cf);
+        div_norm<kNR>(head, norm, rcp_norm, qq, cf, neg_norm);
     }
     // phase 1 for kModeU: the quotient from below, q_m = qq's low word and hi = hi32(q_m) (no
     // fix-up: u = head - q_m * norm in [0, 2 norm) goes to the u-domain tables as it is)
-    template <bool kJ4>
-    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double magic_m1) {
+    // kNormSmall: the estimate divides x' = (H - qh norm) 2^32 + lo after the exact high step
+    // (div_hi, rcp_norm rounded up): x' / norm in [2^32, 2^33), so q_m - qh 2^32 is too, and u is
+    // the same low-word product (x' and head agree in their low words)
+    template <bool kJ4, int kNR = kNormStd>
+    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double magic_m1,
+                                                 double neg_norm = 0.0) {
         form_window();
         P8 -= static_cast<int32_t>(renorm_up8<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
@@ -894,12 +979,15 @@ struct DecChain {
         // the magic: one 64-bit move per step)
         double hd;
         asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
+        uint32_t qh = 0;
+        if constexpr (kNR == kNormSmall) qh = div_hi(hd, rcp_norm, neg_norm);
         const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
         double tq;
         asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(xd), "s"(rcp_norm), "v"(magic_m1));
         const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(tq));  // q_m + 0x43300000'00000000
         cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
-        qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
+        if constexpr (kNR == kNormSmall) qq = mk64(hi32(raw) + qh - 0x43300000u, lo32(raw));
+        else qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
     }
     // the u-domain icdf: bucket u >> shift -> threshold words (w1, w2) with s0 in w1's low bits
     // (kDecUNbMax), the virtual symbol v = s0 + [rx > w1] + [rx > w2] for rx = u << rshift, then
@@ -995,7 +1083,8 @@ struct DecChain {
 // symbol's row; kModeU: kModeRows over u = head - q_m * norm, no quotient fix-up).
 // kP24: every mass is below 2^24 (DecChain::update).  kJ4: some pop can pull 4 bytes (kmax = 4).
 // kVar: chunk c decodes vlen[c] <= chunk_len symbols into the start of its stride (staged output).
-template <typename Sym, int SPP, int kMode, bool kP24, bool kJ4, bool kVar = false>
+// kNR: the norm range (div_norm, renorm_div_u; kNormBig never has the u-domain tables).
+template <typename Sym, int SPP, int kMode, bool kP24, bool kJ4, bool kVar = false, int kNR = kNormStd>
 __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                       const uint64_t* __restrict__ offsets,
                                                       const uint32_t* __restrict__ lens, uint64_t chunk_len,
@@ -1039,8 +1128,11 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const int nunit = static_cast<int>((nvalid + U - 1) / U);
     const uint64_t L = t.L;
     const uint32_t hL8 = renorm_screen(L);
+    static_assert(!(kNR == kNormBig && kMode == kModeU), "u spans [0, 2 norm): 32 bits only below 2^31");
+    static_assert(!(kNR == kNormSmall && kJ4), "norm < 2^16: p K >= 2^40, at most two bytes per pop");
     const uint32_t norm = t.norm;
-    const double rcp_norm = t.rcp_norm;
+    const double rcp_norm = t.rcp_norm;  // (kNormSmall: rounded up)
+    const double neg_norm = -static_cast<double>(norm);
     // 2^52 - 1 in a VGPR pair for the whole kernel (opaque, so it is not rematerialised per step)
     double magic_m1;
     asm("" : "=v"(magic_m1) : "0"(4503599627370495.0));
@@ -1093,11 +1185,11 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                         // so the LDS round trip starts sooner (decode -6% in a same-box A/B,
                         // DESIGN.md §3.1)
                         __builtin_amdgcn_s_setprio(2);
-                        ch.template renorm_div_u<kJ4>(L, hL8, norm, rcp_norm, magic_m1);
+                        ch.template renorm_div_u<kJ4, kNR>(L, hL8, norm, rcp_norm, magic_m1, neg_norm);
                         ch.lookup_u(shift, 32u - shift);
                         __builtin_amdgcn_s_setprio(0);
                     } else {
-                        ch.template renorm_div<kJ4>(L, hL8, norm, rcp_norm);
+                        ch.template renorm_div<kJ4, kNR>(L, hL8, norm, rcp_norm, neg_norm);
                         if constexpr (kFar) {
                             ch.lookup(shift);
                             if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(lcum);

@@ -258,14 +258,25 @@ struct DevBuf {
     hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
 };
 
+// 1/d rounded UP (fma(r, d, -1) is the exact sign of r d - 1): kNormSmall's exact high division
+// step (ans_fast.hpp div_hi) needs r >= 1/d, and r - 1/d < 2^-52 / d keeps its estimates as
+// tight as fl(1/d)'s
+static double rcp_up(uint32_t d) {
+    double r = 1.0 / static_cast<double>(d);
+    while (std::fma(r, static_cast<double>(d), -1.0) < 0.0) r = std::nextafter(r, 2.0);
+    return r;
+}
+
 // Derives the fast-path tables (ans_table.hpp FastTable) when the table qualifies:
-// 2^16 <= norm <= 2^31 (f64 quotient estimate) and nsym <= 65536.  Up to 256
+// nsym <= 65536 with 2^16 <= norm <= 2^31 (f64 quotient estimate), or nsym <= 256
+// at any other norm (the LDS kernels' kNormSmall / kNormBig division).  Up to 256
 // symbols the rows and decode buckets are staged in LDS; above, the encoder reads its rows
 // from global memory and decoding uses the generic kernel.
 int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const DevTable& t = gt->t;
     FastTable ft{};
-    if (!t.fast || t.nsym > 65536) {
+    const uint32_t nr = t.fast ? fast::kNormStd : (t.norm < (1u << 16) ? fast::kNormSmall : fast::kNormBig);
+    if (t.nsym > (nr == fast::kNormStd ? 65536u : 256u)) {
         gt->ft = ft;
         return ANS_OK;
     }
@@ -276,7 +287,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     std::vector<uint32_t> kmax_row(nsym + 1, 0);
     for (uint32_t s = 0; s <= nsym; ++s) {
         const uint64_t m = s < nsym ? cat.masses[s] : 0;
-        enc[s] = EncRow{m ? 1.0 / static_cast<double>(m) : 0.0, static_cast<uint32_t>(m),
+        const double rcp = nr == fast::kNormSmall ? rcp_up(static_cast<uint32_t>(m)) : 1.0 / static_cast<double>(m);
+        enc[s] = EncRow{m ? rcp : 0.0, static_cast<uint32_t>(m),
                         s < nsym ? static_cast<uint32_t>(cat.cummasses[s]) : t.norm};
         if (!m) continue;
         const u128 pK = static_cast<u128>(m) * t.K;
@@ -344,7 +356,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             }
             return lo;
         };
-        uint32_t us = 0;
+        uint32_t us = 1;  // (rx = u << (32 - us) must stay a 32-bit shift)
         while (((n2 - 1) >> us) + 1 > fast::kDecUNbMax) ++us;
         const uint32_t nbu = static_cast<uint32_t>(((n2 - 1) >> us) + 1);
         uimg.assign(fast::kDecTableBytes, 0);
@@ -521,9 +533,12 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_lds_bytes = static_cast<uint32_t>((ft.dec_cum_off + cum_bytes + 15) & ~size_t(15));
     ft.kmax = kmax;
     ft.pmax = pmax;
+    ft.nr = nr;
+    // k_decode's 24-bit high-word product needs hi32(q) < 2^24 too: q < 2^64 / norm
+    ft.p24 = pmax < (1u << 24) && t.norm > 256 ? 1u : 0u;
     ft.K = t.K;
     ft.L = t.L;
-    ft.rcp_norm = t.rcp_norm;
+    ft.rcp_norm = nr == fast::kNormSmall ? rcp_up(t.norm) : t.rcp_norm;
     const size_t enc_b = sizeof(EncRow) * enc.size(), dec_b = ft.dec_cum_off;  // buckets + s0 array
     const size_t decg_b = sizeof(DecBucketG) * decg.size();
     const size_t o_dec = (enc_b + 255) & ~size_t(255), o_cum = o_dec + ((dec_b + 255) & ~size_t(255));

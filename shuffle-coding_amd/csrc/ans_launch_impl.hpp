@@ -347,11 +347,21 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
 #undef ENCV2
             }
         } else {  // LDS rows (ans_fast.hpp k_encode, kVar)
-#define ENCL(KM, K32) fast::k_encode<Sym, KM, K32, false, true><<<grid, fast::kBlock, fast::kEncSharedBytes, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
-            switch (ft.kmax) {
-            case 1: case 2: if (k32) ENCL(2, true); else ENCL(2, false); break;
-            case 3: if (k32) ENCL(3, true); else ENCL(3, false); break;
-            default: if (k32) ENCL(4, true); else ENCL(4, false); break;
+#define ENCL(KM, K32, NR) fast::k_encode<Sym, KM, K32, false, true, NR><<<grid, fast::kBlock, fast::kEncSharedBytes, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
+            if (ft.nr == fast::kNormSmall) {  // (kmax <= 2, K >= 2^40)
+                ENCL(2, false, fast::kNormSmall);
+            } else if (ft.nr == fast::kNormBig) {  // (K < 2^25)
+                switch (ft.kmax) {
+                case 1: case 2: ENCL(2, true, fast::kNormBig); break;
+                case 3: ENCL(3, true, fast::kNormBig); break;
+                default: ENCL(4, true, fast::kNormBig); break;
+                }
+            } else {
+                switch (ft.kmax) {
+                case 1: case 2: if (k32) ENCL(2, true, fast::kNormStd); else ENCL(2, false, fast::kNormStd); break;
+                case 3: if (k32) ENCL(3, true, fast::kNormStd); else ENCL(3, false, fast::kNormStd); break;
+                default: if (k32) ENCL(4, true, fast::kNormStd); else ENCL(4, false, fast::kNormStd); break;
+                }
             }
 #undef ENCL
         }
@@ -359,6 +369,53 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
         HIP_TRY(hipFreeAsync(mem, s));
         HIP_TRY(err);
         return ANS_OK;
+    }
+}
+
+// k_decode's template arguments for a <= 256-symbol table: only the combinations a table can
+// select are instantiated.  u8 (U = 16) takes half-unit points exactly when kmax = 4, wider
+// symbols never (U * 4 <= 60); the u-domain tables are built for u8 symbols' kernels only (the
+// wider-symbol instantiations keep kModeRows: fewer kernels to compile); kNormSmall never pulls
+// more than two bytes (kmax <= 2) and kNormBig runs without the 24-bit product.
+// go(spp, mode, p24, j4, nr) receives each as a std::integral_constant.
+template <typename Sym, typename Go>
+void launch_lds_decode(const FastTable& ft, Go&& go) {
+    using std::integral_constant;
+    constexpr int U = 16 / sizeof(Sym);
+    constexpr bool kHalf = U * 4 > 60;
+    constexpr int kU = sizeof(Sym) == 1 ? fast::kModeU : fast::kModeRows;
+    auto modes = [&](auto spp, auto p24, auto j4, auto nr) {
+        if (ft.dec_far) {
+            go(spp, integral_constant<int, fast::kModeFar>{}, p24, j4, nr);
+            return;
+        }
+        if constexpr (decltype(nr)::value != fast::kNormBig) {
+            if (ft.dec_u) {
+                go(spp, integral_constant<int, kU>{}, p24, j4, nr);
+                return;
+            }
+        }
+        go(spp, integral_constant<int, fast::kModeRows>{}, p24, j4, nr);
+    };
+    auto points = [&](auto p24, auto nr) {
+        if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
+            if constexpr (kHalf && decltype(nr)::value != fast::kNormSmall)
+                modes(integral_constant<int, U / 2>{}, p24, std::true_type{}, nr);
+        } else if (kHalf || ft.kmax < 4 || decltype(nr)::value == fast::kNormSmall) {
+            modes(integral_constant<int, U>{}, p24, std::false_type{}, nr);
+        } else {
+            if constexpr (!kHalf && decltype(nr)::value != fast::kNormSmall)
+                modes(integral_constant<int, U>{}, p24, std::true_type{}, nr);
+        }
+    };
+    if (ft.nr == fast::kNormSmall) {
+        if (ft.p24) points(std::true_type{}, integral_constant<int, fast::kNormSmall>{});
+        else points(std::false_type{}, integral_constant<int, fast::kNormSmall>{});
+    } else if (ft.nr == fast::kNormBig) {
+        points(std::false_type{}, integral_constant<int, fast::kNormBig>{});
+    } else {
+        if (ft.p24) points(std::true_type{}, integral_constant<int, fast::kNormStd>{});
+        else points(std::false_type{}, integral_constant<int, fast::kNormStd>{});
     }
 }
 
@@ -394,28 +451,11 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
         } else {  // LDS buckets (ans_fast.hpp k_decode, kVar)
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nchunks + fast::kDecBlock - 1) / fast::kDecBlock);
-            constexpr int U = 16 / sizeof(Sym);
-#define DECV(SPP, MODE, P24, J4) fast::k_decode<Sym, SPP, MODE, P24, J4, true><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
-#define DECV_P(SPP, MODE, J4) if (ft.pmax < (1u << 24)) DECV(SPP, MODE, true, J4); else DECV(SPP, MODE, false, J4)
-            // the u-domain tables are built for u8 symbols' kernels only (the wider-symbol
-            // instantiations of a <= 256-symbol table keep kModeRows: fewer kernels to compile)
-            constexpr int kU = sizeof(Sym) == 1 ? fast::kModeU : fast::kModeRows;
-#define DECV_M(SPP, J4) if (ft.dec_far) { DECV_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DECV_P(SPP, kU, J4); } else { DECV_P(SPP, fast::kModeRows, J4); }
-            // only the combinations a table can select are instantiated: u8 (U = 16) takes
-            // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
-            constexpr bool kHalf = U * 4 > 60;
-            if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
-                if constexpr (kHalf) { DECV_M(U / 2, true); }
-            } else if constexpr (kHalf) {  // kmax <= 3
-                DECV_M(U, false);
-            } else if (ft.kmax >= 4) {
-                DECV_M(U, true);
-            } else {
-                DECV_M(U, false);
-            }
-#undef DECV_M
-#undef DECV_P
-#undef DECV
+#define DEC(SPP, MODE, P24, J4, NR) fast::k_decode<Sym, SPP, MODE, P24, J4, true, NR><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen)
+            launch_lds_decode<Sym>(ft, [&](auto spp, auto mode, auto p24, auto j4, auto nr) {
+                DEC(decltype(spp)::value, decltype(mode)::value, decltype(p24)::value, decltype(j4)::value, decltype(nr)::value);
+            });
+#undef DEC
         }
         k_unstage<Sym><<<grid_for(units), kBlock, 0, s>>>(stage, span, nchunks, lpad, out);
         const hipError_t err = hipGetLastError();  // free the staging buffer on every path
@@ -464,11 +504,22 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         const size_t lds = fast::kEncSharedBytes;  // rows (LDS-row kernels) + ring
         const bool k32 = ft.K < (1ull << 32);
 #define ENC(KM, K32, G) fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+#define ENCN(KM, K32, NR) fast::k_encode<Sym, KM, K32, false, false, NR><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
 #define ENC_KMAX(G)                                                   \
+        if (!(G) && ft.nr == fast::kNormSmall) {                      \
+            ENCN(2, false, fast::kNormSmall);                         \
+        } else if (!(G) && ft.nr == fast::kNormBig) {                 \
+            switch (ft.kmax) {                                        \
+            case 1: case 2: ENCN(2, true, fast::kNormBig); break;     \
+            case 3: ENCN(3, true, fast::kNormBig); break;             \
+            default: ENCN(4, true, fast::kNormBig); break;            \
+            }                                                         \
+        } else {                                                      \
         switch (ft.kmax) {                                            \
         case 1: case 2: if (k32) ENC(2, true, G); else ENC(2, false, G); break; \
         case 3: if (k32) ENC(3, true, G); else ENC(3, false, G); break; \
         default: if (k32) ENC(4, true, G); else ENC(4, false, G); break; \
+        }                                                             \
         }
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
@@ -487,6 +538,7 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
             ENC_KMAX(false)
         }
 #undef ENC_KMAX
+#undef ENCN
 #undef ENC
         HIP_TRY(hipGetLastError());
     }
@@ -528,7 +580,6 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
     const uint64_t nfull = (lds_table || global_table) ? n / chunk_len : 0;
     if (nfull) {
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
-        constexpr int U = 16 / sizeof(Sym);
         if (global_table) {
             if constexpr (sizeof(Sym) > 1) {
                 const unsigned wgrid = static_cast<unsigned>((nfull + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
@@ -550,24 +601,10 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
             const unsigned dgrid = static_cast<unsigned>((nfull + fast::kDecBlock - 1) / fast::kDecBlock);
-#define DEC(SPP, MODE, P24, J4) fast::k_decode<Sym, SPP, MODE, P24, J4><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
-#define DEC_P(SPP, MODE, J4) if (ft.pmax < (1u << 24)) DEC(SPP, MODE, true, J4); else DEC(SPP, MODE, false, J4)
-            constexpr int kU = sizeof(Sym) == 1 ? fast::kModeU : fast::kModeRows;  // (as in launch_staged_decode)
-#define DEC_M(SPP, J4) if (ft.dec_far) { DEC_P(SPP, fast::kModeFar, J4); } else if (ft.dec_u) { DEC_P(SPP, kU, J4); } else { DEC_P(SPP, fast::kModeRows, J4); }
-            // only the combinations a table can select are instantiated: u8 (U = 16) takes
-            // half-unit points exactly when kmax = 4, wider symbols never (U * 4 <= 60)
-            constexpr bool kHalf = U * 4 > 60;
-            if (kHalf && U * ft.kmax > 60) {  // (kmax = 4)
-                if constexpr (kHalf) { DEC_M(U / 2, true); }
-            } else if constexpr (kHalf) {  // kmax <= 3
-                DEC_M(U, false);
-            } else if (ft.kmax >= 4) {
-                DEC_M(U, true);
-            } else {
-                DEC_M(U, false);
-            }
-#undef DEC_M
-#undef DEC_P
+#define DEC(SPP, MODE, P24, J4, NR) fast::k_decode<Sym, SPP, MODE, P24, J4, false, NR><<<dgrid, fast::kDecBlock, lds, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini)
+            launch_lds_decode<Sym>(ft, [&](auto spp, auto mode, auto p24, auto j4, auto nr) {
+                DEC(decltype(spp)::value, decltype(mode)::value, decltype(p24)::value, decltype(j4)::value, decltype(nr)::value);
+            });
 #undef DEC
         }
         HIP_TRY(hipGetLastError());
@@ -659,7 +696,7 @@ int launch_sample(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_l
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
     if (nchunks == 0) return ANS_OK;
     Sym* out = static_cast<Sym*>(d_syms);
-    if (gt->ft.usable && gt->ft.dec_usable) {  // the fast decoder's LDS tables (ans_fast.hpp k_sample)
+    if (gt->ft.usable && gt->ft.dec_usable && gt->ft.nr == fast::kNormStd) {  // the fast decoder's LDS tables (ans_fast.hpp k_sample)
         const unsigned dgrid = static_cast<unsigned>((nchunks + fast::kDecBlock - 1) / fast::kDecBlock);
         fast::k_sample<Sym><<<dgrid, fast::kDecBlock, gt->ft.dec_lds_bytes, s>>>(gt->ft, seed, n, chunk_len, nchunks, out);
         HIP_TRY(hipGetLastError());

@@ -94,7 +94,9 @@ struct FastTable {
     uint64_t K;
     uint64_t L;
     double rcp_norm;
-    uint32_t usable;      // encode fast path available (2^16 <= norm <= 2^31)
+    uint32_t usable;      // fast paths available (2^16 <= norm <= 2^31, or nsym <= 256 at any norm)
+    uint32_t nr;          // norm range: fast::kNormStd / kNormSmall / kNormBig (ans_fast.hpp)
+    uint32_t p24;         // k_decode's 24-bit high-word product applies (pmax < 2^24, norm > 2^8)
     uint32_t enc_global;  // rows read from global memory (nsym > 256; ans_fast.hpp kGlobalRows)
     uint32_t dec_usable;  // decode fast path available (nsym <= 256: buckets in LDS)
     uint32_t dec_global;  // decode fast path for nsym > 256 (k_decode_g, buckets in global memory)

@@ -143,24 +143,49 @@ def test_gpu_dense_set_edge_cases():
         assert len(data) == 0 and len(z.decode(data, offsets, lens, 64)) == 0
 
 
+def _dataset_masses(nums, graphs, directed, loops, table):
+    """The dataset's Bernoulli: plain_erdos_renyi's (norm 2^28, src/graph_codec.rs:399-401), or
+    DatasetStats::unlabelled's Bernoulli::new(total_edges, total_possible_edges)
+    (src/benchmark.rs:550-557), whose norm is below 2^16 for a set of small graphs."""
+    if table == "er_2^28":
+        return _er_masses(0.08)
+    possible = sum(len(orc.all_edge_indices(n, directed, loops)) if n <= 400 else 0 for n in nums)
+    edges = sum(len(e) for e in graphs)
+    return [possible - edges, edges], edges
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("directed,loops", [(False, False), (True, True)])
-def test_gpu_graph_dataset_bit_exact(directed, loops):
+@pytest.mark.parametrize("table", ["er_2^28", "dataset_counts"])
+def test_gpu_graph_dataset_bit_exact(directed, loops, table):
     """A dataset under one Bernoulli (GraphDatasetParamCodec + ErdosRenyiParamCodec,
-    src/param_codec.rs:171-199,243-293): graph g's stream is the reference message of that
-    graph's edge set alone; decoding returns every graph's edges in alphabet order."""
+    src/param_codec.rs:171-199,243-293): graph g's stream is the oracle's message of that graph's
+    dense edge vector alone, and the host ErdosRenyi push of the graph; decoding returns every
+    graph's edges in alphabet order.  dataset_counts (norm ~4e4 < 2^16) takes the LDS fast
+    kernels' kNormSmall division (ans_fast.hpp)."""
     rng = np.random.default_rng(11 + directed)
-    nums = [int(x) for x in rng.integers(0, 60, 80)] + [0, 1, 2, 150]
+    top = 60 if table == "er_2^28" else 40  # (a counts table of these graphs stays below 2^16)
+    nums = [int(x) for x in rng.integers(0, top, 80)] + [0, 1, 2, 100 if directed else 150]
     p = 0.08
-    masses, mass = _er_masses(p)
     graphs = [_random_graph(rng, n, p, directed, loops) for n in nums]
-    ds = A.GpuDenseSets(A.Gpu(0), A.Bernoulli(mass, NORM), directed, loops)
+    masses, mass = _dataset_masses(nums, graphs, directed, loops, table)
+    norm = int(sum(masses))
+    if table == "dataset_counts":
+        assert norm < (1 << 16)
+        gt = A.GpuTable(A.Gpu(0), A.Categorical(masses))
+        assert gt.paths() & A.ANS_PATH_ENC_LDS and gt.paths() & A.ANS_PATH_DEC_LDS
+    ds = A.GpuDenseSets(A.Gpu(0), A.Bernoulli(mass, norm), directed, loops)
     data, offsets, lens = ds.encode(nums, graphs)
     for g, (n, e) in enumerate(zip(nums, graphs)):
-        er = A.ErdosRenyi(A.Bernoulli(mass, NORM), n, directed, loops)
+        dense = orc.dense_set(e, n, directed, loops)
+        od, _, _ = orc.encode_chunks(masses, dense, max(len(dense), 1))
+        want = od.tobytes() if len(dense) else bytes(orc.Message.zeros().flatten())
+        got = data[int(offsets[g]):int(offsets[g] + lens[g])].tobytes()
+        assert got == want, g
+        er = A.ErdosRenyi(A.Bernoulli(mass, norm), n, directed, loops)
         m = A.Message.zeros()
         er.push(m, [tuple(map(int, x)) for x in e])
-        assert data[int(offsets[g]):int(offsets[g] + lens[g])].tobytes() == m.flatten(), g
+        assert got == m.flatten(), g
     back = ds.decode(nums, data, offsets, lens, cap=5)  # too small: the second pass sizes it
     for g, (n, e) in enumerate(zip(nums, graphs)):
         want = _alphabet_sorted(e, n, directed, loops) if len(e) else np.zeros((0, 2), np.uint32)
