@@ -323,8 +323,10 @@ int ans_gpu_independent_encode_chunks(ans_gpu_tableset *ts, const uint32_t *tabl
 int ans_gpu_independent_decode_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const uint8_t *in,
                                       uint64_t in_len, const uint64_t *offsets, const uint64_t *lens, uint64_t n,
                                       uint64_t chunk_len, int gen_kind, uint64_t seed, void *out, int sym_bytes);
-/* 1 (fast kernels: every table has <= 256 symbols and norm in [2^16, 2^31], at most 31 tables),
- * 2 (the same, with rows of near-certain symbols that take the voted exact renorm), 0 (exact only) */
+/* 1 (fast kernels: every table has <= 256 symbols, the norms all in [2^16, 2^31], all below
+ * 2^16 or all in (2^31, 2^32), and at most 15 tables: 257 encoder rows of 32 B per table beside
+ * the 32-KiB stream ring in 160 KiB of LDS), 2 (the same, with rows of near-certain symbols that
+ * take the voted exact renorm), 0 (exact kernels only: any other set) */
 int ans_gpu_tableset_fast(const ans_gpu_tableset *ts, int *fast);
 
 /* Device-resident 4b calls (replace the bulk IID::push / pop and Independent::push / pop of

@@ -966,28 +966,37 @@ struct DecChain {
     // kNormSmall: the estimate divides x' = (H - qh norm) 2^32 + lo after the exact high step
     // (div_hi, rcp_norm rounded up): x' / norm in [2^32, 2^33), so q_m - qh 2^32 is too, and u is
     // the same low-word product (x' and head agree in their low words)
-    template <bool kJ4, int kNR = kNormStd>
-    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double magic_m1,
-                                                 double neg_norm = 0.0) {
+    //
+    // r05: the estimate lands in the binade [2^49, 2^50), whose ulp is 1/8: t = fma(x, 1/(8 norm),
+    // 2^49 - 1/8) holds q_m in its 52 mantissa bits exactly as 2^52 - 1 with 1/norm did (the same
+    // rounding, scaled by the exact power 2^-3), but the raw high word is 0x43000000 + hi32(q_m):
+    // its low 24 bits ARE hi32(q_m), which is all that update<kP24>'s v_mad_u32_u24 reads, so the
+    // v_and that cleared the exponent (0x433: bits 20-21 set) goes (kP24 only; decode -1 VALU per
+    // symbol).  rcp8 = rcp_norm / 8 (exact).
+    template <bool kJ4, int kNR = kNormStd, bool kP24 = false>
+    __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double rcp8,
+                                                 double magic, double neg_norm = 0.0) {
         form_window();
         P8 -= static_cast<int32_t>(renorm_up8<kJ4>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        // qest_m1 with 1/norm from its SGPR pair (an asm "v" operand copied it into a VGPR pair
-        // every step) and the magic 2^52 - 1 from a loop-invariant VGPR pair as the third
-        // operand of one VOP3 v_fma_f64 (__builtin_fma became v_fmac_f64 on a v_mov_b64 copy of
-        // the magic: one 64-bit move per step)
+        // 1/(8 norm) from its SGPR pair (an asm "v" operand copied it into a VGPR pair every step)
+        // and the magic 2^49 - 1/8 from a loop-invariant VGPR pair as the third operand of one
+        // VOP3 v_fma_f64 (__builtin_fma became v_fmac_f64 on a v_mov_b64 copy of the magic: one
+        // 64-bit move per step)
         double hd;
         asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
         uint32_t qh = 0;
         if constexpr (kNR == kNormSmall) qh = div_hi(hd, rcp_norm, neg_norm);
         const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
         double tq;
-        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(xd), "s"(rcp_norm), "v"(magic_m1));
-        const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(tq));  // q_m + 0x43300000'00000000
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(xd), "s"(rcp8), "v"(magic));
+        const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(tq));  // q_m + 0x43000000'00000000
         cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
-        if constexpr (kNR == kNormSmall) qq = mk64(hi32(raw) + qh - 0x43300000u, lo32(raw));
-        else qq = mk64(hi32(raw) & 0xFFFFFu, lo32(raw));    // q_m < 2^52
+        // (kNormSmall: + qh in the high word, q_m = qh 2^32 + the estimate)
+        const uint32_t hw = kNR == kNormSmall ? hi32(raw) + qh : hi32(raw);
+        if constexpr (kP24) qq = mk64(hw, lo32(raw));  // (low 24 bits: hi32(q_m) < 2^24)
+        else qq = mk64(hw - 0x43000000u, lo32(raw));   // q_m < 2^52 (+ qh 2^32)
     }
     // the u-domain icdf: bucket u >> shift -> threshold words (w1, w2) with s0 in w1's low bits
     // (kDecUNbMax), the virtual symbol v = s0 + [rx > w1] + [rx > w2] for rx = u << rshift, then
@@ -1133,9 +1142,10 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;  // (kNormSmall: rounded up)
     const double neg_norm = -static_cast<double>(norm);
-    // 2^52 - 1 in a VGPR pair for the whole kernel (opaque, so it is not rematerialised per step)
-    double magic_m1;
-    asm("" : "=v"(magic_m1) : "0"(4503599627370495.0));
+    // 2^49 - 1/8 in a VGPR pair for the whole kernel (opaque, so it is not rematerialised per step)
+    double magic_u;
+    asm("" : "=v"(magic_u) : "0"(562949953421311.875));
+    const double rcp8 = rcp_norm * 0.125;
     const uint32_t shift = kMode == kModeU ? t.dec_u_shift : t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
@@ -1185,7 +1195,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                         // so the LDS round trip starts sooner (decode -6% in a same-box A/B,
                         // DESIGN.md §3.1)
                         __builtin_amdgcn_s_setprio(2);
-                        ch.template renorm_div_u<kJ4, kNR>(L, hL8, norm, rcp_norm, magic_m1, neg_norm);
+                        ch.template renorm_div_u<kJ4, kNR, kP24>(L, hL8, norm, rcp_norm, rcp8, magic_u, neg_norm);
                         ch.lookup_u(shift, 32u - shift);
                         __builtin_amdgcn_s_setprio(0);
                     } else {

@@ -630,7 +630,7 @@ struct NoState {
 };
 
 // ====================================================================== Independent<Categorical>
-// A set of T <= kIndMaxTables Categoricals with <= 256 symbols and norm in [2^16, 2^31]
+// A set of T <= kIndMaxTables Categoricals with <= 256 symbols, all in one norm range (kNR)
 // (src/codec.rs:51-92), a table per position (src/codec.rs:366-403), table ids as one byte each.
 //
 // Encoder image (LDS kEncTab, the same bytes in global memory): row (t, s) at t*8224 + 32 s,
@@ -660,7 +660,9 @@ constexpr uint32_t kIndRowOff = 1024;                   // decoder rows after th
 constexpr uint32_t kIndFarBit = 0x200u;
 constexpr uint32_t kIndMaxShift = 22;                   // rshift = 32 - us >= 10
 
-template <bool kRare>
+// kNR (ans_fast.hpp kNormStd / kNormSmall / kNormBig): every table of the set in that norm range;
+// kNormSmall rows carry 1/p rounded up and the headers 1/norm rounded up (the long division).
+template <bool kRare, int kNR = fast::kNormStd>
 struct IndepModel {
     static constexpr bool kTids = true;
     using DecState = NoState;
@@ -693,21 +695,37 @@ struct IndepModel {
         // q = head / p, r = head % p (src/ans.rs:101-102): round(head/p - 1/2), exact unless head/p
         // lies within 2^-4 of an integer; such lanes (and zero-mass rows, rcp 0) take the voted
         // 64-bit remainder (ans_fast.hpp k_encode push_one)
-        uint64_t qb = fast::qest_half(e.head, rcp);
+        // (kNormSmall: on x' = (H - qh p) 2^32 + lo after the exact high step, ans_fast.hpp div_hi;
+        // kNormBig: rows of mass above 2^31 always take the exact branch, ans_fast.hpp k_encode)
+        uint32_t qh = 0;
+        uint64_t qb;
+        if constexpr (kNR == fast::kNormSmall) {
+            double hd;
+            asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(e.head)));
+            qh = fast::div_hi(hd, rcp, -static_cast<double>(mass));
+            const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(e.head)));
+            double t;
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "v"(xd), "v"(rcp), "v"(4503599627370495.5));
+            qb = static_cast<uint64_t>(__double_as_longlong(t));
+        } else {
+            qb = fast::qest_half(e.head, rcp);
+        }
         uint32_t rm = lo32(e.head) - lo32(qb) * mass;
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= mass) != 0, 0)) {
-            if (rm >= mass) {
+        const bool fix = kNR == fast::kNormBig ? (rm >= mass || static_cast<int32_t>(mass) < 0) : rm >= mass;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(fix) != 0, 0)) {
+            if (fix) {
                 if (mass == 0) e.err |= kErrZeroMass;
-                const int64_t r = static_cast<int64_t>(e.head - (qb - 0x4330000000000000ull) * mass);
-                const int64_t d = r < 0 ? -1 : 1;
+                const uint64_t x = kNR == fast::kNormSmall ? mk64(hi32(e.head) - qh * mass, lo32(e.head)) : e.head;
+                const int64_t r = static_cast<int64_t>(x - (qb - 0x4330000000000000ull) * mass);
+                const int64_t d = r < 0 ? -1 : (kNR != fast::kNormBig || r >= static_cast<int64_t>(mass) ? 1 : 0);
                 qb += static_cast<uint64_t>(d);
                 rm = static_cast<uint32_t>(r - d * static_cast<int64_t>(mass));
             }
         }
         // head = norm * q + cdf(x, r) (src/ans.rs:103-104): q < 2^52, hi32(q) = the raw high word's
-        // low 20 bits
+        // low 20 bits (+ qh)
         const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * norm + (cum + rm);
-        e.head = mk64(hi32(lo64) + (hi32(qb) & 0xFFFFFu) * norm, lo32(lo64));
+        e.head = mk64(hi32(lo64) + ((hi32(qb) & 0xFFFFFu) + qh) * norm, lo32(lo64));
     }
     // a zero-mass lane: an out-of-range symbol (src/codec.rs:63) or p == 0 (src/ans.rs:98)
     template <typename Sym>
@@ -743,7 +761,7 @@ struct IndepModel {
         __builtin_amdgcn_sched_barrier(0);
         uint64_t qq;
         uint32_t cf;
-        fast::div_norm(ch.head, norm, rcp_norm, qq, cf);
+        fast::div_norm<kNR>(ch.head, norm, rcp_norm, qq, cf, -static_cast<double>(norm));
         const uint64_t cc = lds_ld64(bkt + ((cf >> us) << 3));
         __builtin_amdgcn_s_setprio(0);
         const uint32_t rx = cf << rsh;

@@ -87,6 +87,58 @@ def test_independent_fast_mixed_norms(gpu, dtype, L):
         _check_indep(ts, tables, tids, syms, L, dtype, kind, seed)
 
 
+def _small_norm_tables(rng):
+    """Count-built tables below 2^16 (src/benchmark.rs:549-578): a dataset edge Bernoulli, label
+    counts with an absent label, Bernoulli::new(1, 2) (src/param_codec.rs:273), a 256-symbol one."""
+    return [np.array([31000, 3400], np.uint64), np.array([2395, 345, 593, 0, 23, 12, 2], np.uint64),
+            np.array([1, 1], np.uint64), rng.integers(1, 200, size=256).astype(np.uint64),
+            np.array([65000, 1, 1, 7], np.uint64)]
+
+
+def _big_norm_tables(rng):
+    """Norms in (2^31, 2^32), a mass above 2^31 among them."""
+    t = [rng.integers(1 << 23, 1 << 24, size=256).astype(np.uint64),
+         np.array([(1 << 31) + 12345, 1, 77, 1 << 30], np.uint64),
+         np.array([(1 << 32) - 2, 1], np.uint64)]
+    t[0] = (t[0] * ((1 << 32) - 99) // int(t[0].sum())).astype(np.uint64)
+    return t
+
+
+@pytest.mark.parametrize("which", ["small", "big"])
+@pytest.mark.parametrize("dtype,L", [(np.uint8, 4096), (np.uint8, 128), (np.uint16, 512)])
+def test_independent_fast_norm_ranges(gpu, which, dtype, L):
+    """Sets whose norms all lie below 2^16 (or all in (2^31, 2^32)) take the fast kernels with
+    the long-division (64-bit-checked) quotient of ans_fast.hpp kNormSmall (kNormBig)."""
+    rng = np.random.default_rng(300 + L + len(which))
+    tables = _small_norm_tables(rng) if which == "small" else _big_norm_tables(rng)
+    for m in tables:
+        assert (int(m.sum()) < 1 << 16) if which == "small" else ((1 << 31) < int(m.sum()) < (1 << 32))
+    ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
+    assert ts.fast() in (1, 2)
+    n = 301 * L + 17
+    tids = rng.integers(0, len(tables), size=n).astype(np.uint32)
+    syms = np.zeros(n, np.uint64)
+    for t, m in enumerate(tables):  # uniform over each table's symbols: the rare rows often
+        sel = tids == t
+        syms[sel] = rng.choice(np.flatnonzero(m), size=int(sel.sum()))
+    for kind, seed in [(A.GEN_ZEROS, 0), (A.GEN_RANDOM, 4)]:
+        _check_indep(ts, tables, tids, syms, L, dtype, kind, seed)
+
+
+def test_independent_exact_only_sets(gpu):
+    """Sets the fast kernels decline stay bit-exact on the exact kernels: norms from two ranges in
+    one set, and sixteen 256-symbol tables (16 x 8,224 B of encoder rows pass the LDS)."""
+    rng = np.random.default_rng(77)
+    mixed = [rng.integers(1, 1 << 16, size=256).astype(np.uint64), np.array([3, 5], np.uint64)]
+    sixteen = [rng.integers(1, 1 << 16, size=256).astype(np.uint64) for _ in range(16)]
+    fifteen = sixteen[:15]
+    for tables, fast in [(mixed, 0), (sixteen, 0), (fifteen, 1)]:
+        ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
+        assert ts.fast() == fast, len(tables)
+        tids, syms = _indep_case(rng, tables, 40 * 256)
+        _check_indep(ts, tables, tids, syms, 256, np.uint8)
+
+
 def _renorm_tables():
     """Tables whose pushes, in the order below, leave a head of 2^56 - 2^25 before a push with
     p K = 2^56 - 1, which must take a byte back (see the docstring of the test)."""
