@@ -72,6 +72,7 @@ def parse(argv=None):
     p.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) sub-object")
     p.add_argument("--strong", action="store_true",
                    help="strong scaling: the config's 2^log2n symbols in total, split over the ranks")
+    p.add_argument("--test-fail-rank", type=int, default=None, help=argparse.SUPPRESS)  # tests/test_bench.py only
     return p.parse_args(argv)
 
 
@@ -237,11 +238,11 @@ def workload(ctx, masses, sym_bytes, seed, start, n, L):
     return gt, cap, nchunks, syms, slots, lens, out
 
 
-def timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out, steps, warmup, pre=None):
+def timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out, steps, warmup, pre=None, fail_rank=None):
     """warmup untimed steps, then `steps` steps bracketed by barrier + synchronize on both
     sides; (wall seconds, mean encode ms, mean decode ms, pre()'s result) with HIP events on
     ctx.stream.  pre: work queued just before the warm-up (the dense pass), inside the same
-    failure agreement."""
+    failure agreement.  fail_rank (--test-fail-rank, tests only): that rank's warm-up raises."""
     torch, stream, status = ctx.torch, ctx.stream, ctx.status
 
     def step(ev=None):
@@ -260,8 +261,8 @@ def timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens, out, ste
     try:
         if pre is not None:
             pre_out = pre()
-        if os.environ.get("BENCH_FAIL_RANK") == str(ctx.rank):  # test knob: one rank's launch fails
-            raise RuntimeError("BENCH_FAIL_RANK")
+        if fail_rank == ctx.rank:
+            raise RuntimeError("--test-fail-rank")
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
@@ -559,7 +560,8 @@ def main():
     pre = None if args.no_dense else (lambda: dense_pass(ctx, gt, syms, sym_bytes, n, L, nchunks, slots, cap,
                                                          min(args.steps, 10), max(args.warmup, 20)))
     elapsed, enc_ms, dec_ms, dense_finish = timed_round_trips(ctx, gt, syms, sym_bytes, n, L, slots, cap, lens,
-                                                              out, args.steps, args.warmup, pre=pre)
+                                                              out, args.steps, args.warmup, pre=pre,
+                                                              fail_rank=args.test_fail_rank)
     dense = None if dense_finish is None else dense_finish()
     dense_bad = dense is not None and not dense.pop("ok")
 
@@ -638,8 +640,12 @@ def main():
     ks_ns = None if ks is None else ks.get("avg_ns")
     hbm_frac = achieved / HBM_PEAK_GBS
     # what binds: the VALU issue fraction (PMC instruction count at 4 cycles per wave64
-    # instruction) when it exceeds the HBM fraction, as it does for the integer coding kernels
-    bound = "valu-issue" if (valu and valu["frac_at_2.4GHz"] > hbm_frac) else "hbm"
+    # instruction) when it exceeds the HBM fraction, as it does for the integer coding kernels;
+    # only from PMC counts of this very build (another build's counts name no bound)
+    if valu and valu["pmc_same_build"]:
+        bound = "valu-issue" if valu["frac_at_2.4GHz"] > hbm_frac else "hbm"
+    else:
+        bound = "unknown (no PMC record of this build)"
 
     if rank == 0:
         per_frac = [(r[4] * sym_bytes + r[5]) / (max(r[2], r[3]) * 1e-3) / 1e9 / HBM_PEAK_GBS for r in rows]

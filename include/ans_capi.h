@@ -335,7 +335,12 @@ int ans_gpu_tableset_fast(const ans_gpu_tableset *ts, int *fast);
  * into *d_status as (1u << status) bits (ans_dev_status); asynchronous on `stream` (NULL = the
  * context's).  Decoders read slots (d_offsets NULL) or a dense container at d_in + d_offsets[j].
  * d_tids: the table id of every position, one byte each (sets of at most 256 tables; ids are
- * not range-checked on the device, as the reference would index past its codec vector). */
+ * not range-checked on the device, as the reference would index past its codec vector).
+ * slot_cap is the codec's slot capacity (the _slot_capacity call for chunk_len) for every call,
+ * dense-container decodes included: it bounds the fast kernels' stream positions, and any other
+ * value sends every chunk to the exact kernels.  d_syms, d_tids and d_slots must be 16-byte
+ * aligned (the fast kernels move symbols, table ids and slot pages with 16-B vector loads and
+ * stores; hipMalloc and torch allocations are); a dense container's streams may start anywhere. */
 int ans_gpu_uniform_slot_capacity(uint64_t size, uint64_t chunk_len, uint64_t *slot_cap);
 int ans_gpu_loguniform_slot_capacity(uint32_t excl_max_bits, uint64_t chunk_len, uint64_t *slot_cap);
 int ans_gpu_tableset_slot_capacity(const ans_gpu_tableset *ts, uint64_t chunk_len, uint64_t *slot_cap);

@@ -48,6 +48,7 @@ struct HostPipe {
 
 struct ans_gpu {
     int device;
+    int ncu;  // compute units (launchers size per-CU LDS use by it)
     hipStream_t stream;
     HostPipe* pipe;
     uint64_t batch_bytes;  // symbol bytes per pipeline batch (0 = default)

@@ -1272,7 +1272,9 @@ int ans_gpu_create(int device, ans_gpu** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return ANS_E_DEVICE;
     HIP_TRY(hipSetDevice(device));
-    auto* g = new (std::nothrow) ans_gpu{device, nullptr, nullptr, 0, nullptr, 0};
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
+    auto* g = new (std::nothrow) ans_gpu{device, ncu, nullptr, nullptr, 0, nullptr, 0};
     if (!g) return ANS_E_ALLOC;
     if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
         delete g;

@@ -303,6 +303,18 @@ inline size_t wide_enc_lds(const FastTable& ft) {
     return (ft.enc_sa ? fast::kWideSaBytes : 0) + fast::kWideBBytes + fast::kEncRingBytes + (ft.enc_pack_bytes - ft.enc_pack_ooff);
 }
 
+// k_decode_w's dynamic LDS and its staged compact buckets (ft.dec_c_nlb): the 67.5-KiB ring plus
+// the first buckets, up to the rest of the CU's 160 KiB (C4: 6,016 of 65,704), so one 512-lane
+// workgroup fits per CU.  Measured against two workgroups per CU with the ring alone (four waves
+// per SIMD where a grid has more workgroups than CUs): 2^31 u16 symbols (1,024 workgroups) decode
+// in 8.55 ms staged vs 8.98 ms (profiles/r05_ab_c4_2e31_two_wg_per_cu_rejected.txt; a C4 shard,
+// 256 workgroups, is the same either way): the L2 request rate, not the wave count, binds.
+inline size_t wide_dec_lds(FastTable& ft, unsigned /*wgrid*/, int /*ncu*/) {
+    const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(ft.norm) - 1) >> ft.dec_c_shift) + 1);
+    ft.dec_c_nlb = std::min(nb, fast::kWideDecBktLds);
+    return fast::kWideDecTab + 16ull * ft.dec_c_nlb;
+}
+
 // The staged route applies to the large-alphabet fast kernels (u16 / u32 symbols).
 template <typename Sym>
 bool staged_encode_ok(const ans_gpu_table* gt) {  // large-alphabet or LDS-row encoder
@@ -443,10 +455,13 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
         if (wide) {
           if constexpr (sizeof(Sym) > 1) {
             const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
-            if (ft.dec_c)
-                fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
-            else
+            if (ft.dec_c) {
+                FastTable fw = ft;
+                const size_t wl = wide_dec_lds(fw, wgrid, gt->g->ncu);
+                fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+            } else {
                 fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+            }
           }
         } else {  // LDS buckets (ans_fast.hpp k_decode, kVar)
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
@@ -583,15 +598,17 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
         if (global_table) {
             if constexpr (sizeof(Sym) > 1) {
                 const unsigned wgrid = static_cast<unsigned>((nfull + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
-                // compact buckets: every lookup from L2, no LDS prefix (C4 decode 2.45 -> 2.28 ms:
-                // the shard's 2 waves per SIMD wait on an L2 round trip every step whatever the
-                // prefix covers, and the prefix path's VALU sat on that chain); the ring alone
-                // leaves room for two workgroups per CU when a shard has the chunks for them
+                // compact buckets: no LDS prefix (C4 decode 2.45 -> 2.28 ms: the shard's 2 waves per
+                // SIMD wait on an L2 round trip every step whatever the prefix covers, and the
+                // prefix path's VALU sat on that chain); the first buckets staged in the LDS the
+                // ring leaves (wide_dec_lds: one workgroup per CU)
                 if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0) {
+                    FastTable fw = ft;
+                    const size_t wl = wide_dec_lds(fw, wgrid, gt->g->ncu);
                     if (ft.pmax < (1u << 24))
-                        fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                        fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                     else
-                        fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                        fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
                 }
                 else if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
                     fast::k_decode_w<Sym, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);

@@ -132,6 +132,7 @@ struct FastTable {
     const DecBucketC* dbkt_c;
     uint32_t dec_c;
     uint32_t dec_c_shift;
+    uint32_t dec_c_nlb;  // k_decode_w<kCompact, !kPrefix>: the first buckets staged in LDS (set per launch)
     // k_decode kModeU (ans_fast.hpp): the quotient from below without a fix-up; u = head - q_m*norm
     // in [0, 2 norm) indexes a virtual 512-symbol alphabet whose buckets (width 2^dec_u_shift)
     // all resolve among three candidates.  dec_u_img is the LDS image (fast::kDecTableBytes).

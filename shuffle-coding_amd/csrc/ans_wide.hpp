@@ -529,17 +529,11 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
         uint32_t* lc = reinterpret_cast<uint32_t*>(lds + kWideDecTab + t.dec_w_cum_off);
         for (uint32_t i = threadIdx.x; i <= t.dec_w_nlp + 5; i += kWideDecLanes) lc[i] = t.cum[i];
     }
-    // compact buckets without the prefix (C4): the first nlb buckets are staged in the LDS the
-    // ring leaves (kWideDecBktLds: 6,016 of C4's 65,704), so that share of the lookups issues no
-    // L2 request (the decoder runs at ~0.87 of the L2 gather ceiling)
-    const uint32_t nlb = [&]() -> uint32_t {
-        if constexpr (kCompact && !kPrefix) {
-            const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(t.norm) - 1) >> t.dec_c_shift) + 1);
-            return umin(nb, kWideDecBktLds);
-        } else {
-            return 0;
-        }
-    }();
+    // compact buckets without the prefix (C4): the first nlb = t.dec_c_nlb buckets are staged in
+    // the LDS the ring leaves (up to kWideDecBktLds: 6,016 of C4's 65,704), so that share of the
+    // lookups issues no L2 request (the decoder runs at ~0.87 of the L2 gather ceiling, DESIGN.md
+    // §3.3).  The launcher sizes the dynamic LDS for them (ans_launch_impl.hpp wide_dec_lds).
+    const uint32_t nlb = kCompact && !kPrefix ? t.dec_c_nlb : 0u;
     if constexpr (kCompact && !kPrefix) {
         const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt_c);
         uint4* lb = reinterpret_cast<uint4*>(lds + kWideDecTab);

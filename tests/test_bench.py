@@ -70,10 +70,33 @@ def test_bench_strong_scaling_two_ranks():
 
 @pytest.mark.gpu
 def test_bench_failing_rank_ends_every_rank():
-    """A rank whose launch raises (test knob BENCH_FAIL_RANK) must not leave the other rank in
-    the timed region's barrier: both reach the same failure agreement and exit non-zero, well
+    """A rank whose launch raises (the hidden --test-fail-rank flag) must not leave the other rank
+    in the timed region's barrier: both reach the same failure agreement and exit non-zero, well
     inside the launcher's own timeouts."""
-    r = _two_ranks(["--log2n", "22", "--no-c4"], timeout=100, BENCH_FAIL_RANK="1")
+    r = _two_ranks(["--log2n", "22", "--no-c4", "--test-fail-rank", "1"], timeout=100)
     assert r.returncode != 0
     assert "failed on rank(s) [1]" in r.stderr, r.stderr[-2000:]
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_eight_ranks_one_device():
+    """The driver's 8-GPU scaling launch rehearsed on one device: `bench.py --gpus 8` starts eight
+    ranks (global symbol offsets 0..7 x 2^20, the same rank order and shard layout as on an 8-GPU
+    node), rank 0 prints one JSON line with eight per-rank entries and the C4 sub-object's
+    per-rank spread; gloo carries the barrier and the gather (RCCL needs a GPU per rank)."""
+    r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "8", "--steps", "3", "--warmup", "1", "--log2n", "20",
+                        "--c4-log2n", "18", "--no-cpu-baseline", "--no-dense", "--no-host"],
+                       env={k: v for k, v in dict(os.environ, BENCH_SHARE_DEVICE="1", BENCH_BACKEND="gloo").items()
+                            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")},
+                       capture_output=True, text=True, timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "weak"
+    assert d["config"]["symbols_per_rank"] == [1 << 20] * 8
+    assert d["config"]["symbols_total"] == 8 << 20
+    assert abs(d["value"] - 8 * (1 << 20) / (d["ms_per_step"] * 1e-3) / 2**30) < 0.01 * d["value"]
+    assert d["c4"]["per_rank"]["ms_per_step"]["max"] == d["c4"]["ms_per_step"]
+    assert d["c4"]["workload"].startswith("C4: 2^18 iid u16 symbols per GPU (0.00390625 GiB over 8 GPUs)")
