@@ -328,6 +328,12 @@ int ans_gpu_independent_decode_chunks(ans_gpu_tableset *ts, const uint32_t *tabl
  * the 32-KiB stream ring in 160 KiB of LDS), 2 (the same, with rows of near-certain symbols that
  * take the voted exact renorm), 0 (exact kernels only: any other set) */
 int ans_gpu_tableset_fast(const ans_gpu_tableset *ts, int *fast);
+/* The fast kernels' workgroup layout for this set: 0 (default) picks 1,024-lane workgroups
+ * sharing one LDS table image (the encoder's when it fits 32 KiB, the decoder's when it fits
+ * 28 KiB) for calls of at least (compute units x 1,024) chunks, 256-lane ones below; 256 or
+ * 1,024 force one where that image exists (ANS_E_ARG for 1,024 when neither fits).  The bytes
+ * are the same either way. */
+int ans_gpu_tableset_lanes(ans_gpu_tableset *ts, int lanes);
 
 /* Device-resident 4b calls (replace the bulk IID::push / pop and Independent::push / pop of
  * src/codec.rs:388-399,415-424 on device memory): fixed chunks, chunk j's stream in its slot at

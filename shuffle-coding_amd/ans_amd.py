@@ -99,6 +99,7 @@ SIGNATURES = {
     "ans_gpu_independent_encode_chunks": (ci, [vp, vp, vp, ci, u64, u64, ci, u64, vp, u64, vp, vp, u64p]),
     "ans_gpu_independent_decode_chunks": (ci, [vp, vp, vp, u64, vp, vp, u64, u64, ci, u64, vp, ci]),
     "ans_gpu_tableset_fast": (ci, [vp, ctypes.POINTER(ci)]),
+    "ans_gpu_tableset_lanes": (ci, [vp, ci]),
     "ans_gpu_uniform_slot_capacity": (ci, [u64, u64, ctypes.POINTER(u64)]),
     "ans_gpu_loguniform_slot_capacity": (ci, [ctypes.c_uint32, u64, ctypes.POINTER(u64)]),
     "ans_gpu_tableset_slot_capacity": (ci, [vp, u64, ctypes.POINTER(u64)]),
@@ -946,6 +947,10 @@ class GpuTableSet:
         f = ci(0)
         _check(lib().ans_gpu_tableset_fast(self.h, ctypes.byref(f)), "ans_gpu_tableset_fast")
         return f.value
+
+    def lanes(self, lanes):
+        """The fast kernels' workgroup layout: 0 by call size, 256, or 1024 (one shared table image)."""
+        _check(lib().ans_gpu_tableset_lanes(self.h, lanes), "ans_gpu_tableset_lanes")
 
     def slot_capacity(self, chunk_len):
         c = u64(0)

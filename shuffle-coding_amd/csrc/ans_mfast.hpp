@@ -57,6 +57,21 @@ constexpr uint32_t kDecTab = kDecRingBytes;       // LDS offset of the decoder's
 static_assert(kDecTab % 256 == 0, "tables 256-B aligned");
 constexpr uint32_t kLdsMax = 160 * 1024;
 constexpr uint64_t kMaxMinHead = 1ull << 56;  // src/ans.rs:19
+// r05: the decoder's second layout, as ans_fast.hpp k_decode's: 1,024-lane workgroups (four
+// waves per SIMD where a call has the chains: 2^30 u8 symbols in 4,096-symbol chunks is 1,024
+// chains per CU) sharing ONE table image of at most kDecTabW bytes at LDS offset 0, the ring
+// after it.  The 256-lane layout (ring at 0, tables after it) stays for images that do not fit.
+constexpr int kLanesW = 1024;
+constexpr uint32_t kDecTabW = 28672;
+static_assert(kDecTabW + kDecRows * kLanesW * 4 == kLdsMax, "1,024 rings + the tables = one CU's LDS");
+template <int kL>
+struct DecLayout {
+    static_assert(kL == kLanes || kL == kLanesW, "two layouts");
+    static constexpr uint32_t kRing = kL == kLanes ? 0u : kDecTabW;   // LDS offset of ring row 0
+    static constexpr uint32_t kTab = kL == kLanes ? kDecTab : 0u;     // LDS offset of the model's tables
+    static constexpr uint32_t kRowShift = kL == kLanes ? 10u : 12u;   // log2 of a ring row's bytes
+    static constexpr uint32_t kLds = kL == kLanes ? 0u : kLdsMax;     // (256 lanes: the caller's size)
+};
 
 // encoder error bits (lane-private; reported as ANS_E_* by the skeleton)
 constexpr uint32_t kErrSymbol = 1;    // symbol outside the alphabet (src/codec.rs:63, LogUniform bits >= size)
@@ -65,19 +80,43 @@ constexpr uint32_t kErrNormRange = 4; // Uniform::new(2^(bits-1)) beyond MAX_SIZ
 constexpr uint32_t kErrPulled = 8;    // a take-back reached past the stream's start (generator bytes)
 
 // ====================================================================== encoder
-// The stream's dword i lives in ring row i & 31: LDS ((i & 31) << 10) | 4 lane.
-struct MRing {
-    uint32_t col;
-    __device__ __forceinline__ lds_u32& at(int32_t i) const {
-        const uint32_t a = ((static_cast<uint32_t>(i) << 10) & 0x7C00u) | col;
-        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a));
+// Two layouts, as the decoder's (DecLayout): 256 lanes with the ring at LDS offset 0 and the
+// model's tables after it (kEncTab), or (r05) 1,024 lanes sharing ONE table image of at most
+// kEncTabW bytes at offset 0 with the ring after it, four waves per SIMD where a call has the
+// chains (1,024 per CU).  The stream's dword i lives in ring row i & 31: ((i & 31) << R) | 4 lane,
+// R = log2 of a row's bytes.
+constexpr uint32_t kEncTabW = 32768;
+static_assert(kEncTabW + 32u * kLanesW * 4 == kLdsMax, "1,024 rings + the tables = one CU's LDS");
+template <int kL>
+struct EncLayout {
+    static_assert(kL == kLanes || kL == kLanesW, "two layouts");
+    static constexpr uint32_t kRing = kL == kLanes ? 0u : kEncTabW;
+    static constexpr uint32_t kTab = kL == kLanes ? kEncTab : 0u;
+    static constexpr uint32_t kRowShift = kL == kLanes ? 10u : 12u;
+    static constexpr uint32_t kRowMask = 31u << kRowShift;
+    // the row address of stream bit position pos8 (dword pos8 >> 5), without the ring base
+    static __device__ __forceinline__ uint32_t row_of(uint32_t pos8, uint32_t col) {
+        if constexpr (kL == kLanes) return (shl16<5>(pos8) & kRowMask) | col;  // (fits 16 bits)
+        else return ((pos8 << (kRowShift - 5)) & kRowMask) | col;
     }
 };
 
-// The byte funnel of ans_fast.hpp (FunnelT) on the 256-lane ring, plus take_back: pos8 = 8 *
-// stream bytes so far; X holds dword pos/4 with its pos&3 written bytes at the bottom; every
-// dword below it is in the ring.
-struct MFunnel {
+template <int kL>
+struct MRingT {
+    using Lay = EncLayout<kL>;
+    uint32_t col;
+    __device__ __forceinline__ lds_u32& at(int32_t i) const {
+        const uint32_t a = ((static_cast<uint32_t>(i) << Lay::kRowShift) & Lay::kRowMask) | col;
+        return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(a + Lay::kRing));
+    }
+};
+
+// The byte funnel of ans_fast.hpp (FunnelT) on the ring, plus take_back: pos8 = 8 * stream bytes
+// so far; X holds dword pos/4 with its pos&3 written bytes at the bottom; every dword below it
+// is in the ring.  addr: the ring address (less the ring base) of dword pos/4.
+template <int kL>
+struct MFunnelT {
+    using Lay = EncLayout<kL>;
     uint32_t X, pos8, neg8, addr, col;
 
     __device__ __forceinline__ void push(uint32_t lo, uint32_t k8) {
@@ -85,10 +124,10 @@ struct MFunnel {
         asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
         asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d0) : "v"(lo), "v"(pos8), "v"(xv));
         asm("v_lshrrev_b32 %0, %1, %2" : "=v"(d1) : "v"(neg8), "v"(lo));
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = d0;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + Lay::kRing)) = d0;
         pos8 += k8;
         neg8 -= k8;
-        const uint32_t a = (shl16<5>(pos8) & 0x7C00u) | col;  // ((pos8 >> 5) & 31) << 10
+        const uint32_t a = Lay::row_of(pos8, col);
         X = a != addr ? d1 : d0;
         addr = a;
     }
@@ -96,9 +135,9 @@ struct MFunnel {
     __device__ __forceinline__ uint32_t take_back() {
         pos8 -= 8;
         neg8 += 8;
-        const uint32_t a = (shl16<5>(pos8) & 0x7C00u) | col;
+        const uint32_t a = Lay::row_of(pos8, col);
         if (a != addr) {  // the byte lies in the dword below, which is in the ring
-            X = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a));
+            X = *reinterpret_cast<const lds_u32*>(static_cast<uintptr_t>(a + Lay::kRing));
             addr = a;
         }
         return (X >> (pos8 & 31u)) & 0xFFu;
@@ -107,14 +146,15 @@ struct MFunnel {
     __device__ __forceinline__ void finish() {
         uint32_t xv;
         asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(xv) : "v"(X), "v"(pos8));
-        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)) = xv;
+        *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr + Lay::kRing)) = xv;
     }
 };
 
 // completed pages leave in aligned 128-B pairs (ans_fast.hpp PageOut)
 struct MPageOut {
     uint4 h0, h1, h2, h3;
-    __device__ __forceinline__ void page(const MRing& ring, uint32_t p, uint8_t* dst) {
+    template <class Ring>
+    __device__ __forceinline__ void page(const Ring& ring, uint32_t p, uint8_t* dst) {
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = ring.at(static_cast<int32_t>(16 * p + i));
@@ -148,9 +188,10 @@ struct MPageOut {
 };
 
 // One chain's encoder state, handed to the model's push.
-struct EncLane {
+template <int kL>
+struct EncLaneT {
     uint64_t head;
-    MFunnel f;
+    MFunnelT<kL> f;
     uint32_t err;
     // push the head's low 8k8/8 bytes (up to 8) and drop them from the head
     __device__ __forceinline__ void emit(uint32_t k8) {
@@ -174,6 +215,9 @@ struct EncLane {
         }
     }
 };
+using MRing = MRingT<kLanes>;
+using MFunnel = MFunnelT<kLanes>;
+using EncLane = EncLaneT<kLanes>;
 
 // 8 * #{j >= 1 : head >> 8j >= pK} (src/ans.rs:246-253), exact (the voted slow paths)
 __device__ __forceinline__ uint32_t bytes_out8_exact(uint64_t head, uint64_t pK) {
@@ -217,36 +261,40 @@ __device__ __forceinline__ void unit_put(uint4& v, int j, uint32_t lo, uint32_t 
 // The encode skeleton.  Chunk c (< nfull: every chunk holds chunk_len symbols, chunk_len * w a
 // multiple of 128) is IID / Independent::push of its symbols last first (src/codec.rs:388-391,
 // 415-420) from the chunk's initial message, then flatten (src/ans.rs:255-260), into slot c.
-// Symbols (and table ids) come in 128-B groups per lane, walked last to first; a point (the
+// Symbols (and table ids) come in 128-B groups per lane (64 B for 1,024 lanes), walked last to first; a point (the
 // page flush) precedes every SPP symbols, which emit at most 64 bytes between them.
-template <class Model, typename Sym, int SPP>
-__global__ __launch_bounds__(kLanes, 2) void k_menc(Model md, const Sym* __restrict__ syms,
-                                                     const uint8_t* __restrict__ tids, uint64_t chunk_len,
-                                                     uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
-                                                     uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
-                                                     ChunkInit ini) {
+// kL: the layout (EncLayout; the model's tables must be built for it, Model::kTabE).
+template <class Model, typename Sym, int SPP, int kL = kLanes>
+__global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, const Sym* __restrict__ syms,
+                                                                   const uint8_t* __restrict__ tids, uint64_t chunk_len,
+                                                                   uint64_t nfull, uint8_t* __restrict__ slots,
+                                                                   uint64_t slot_cap, uint32_t* __restrict__ lens,
+                                                                   uint32_t* __restrict__ status, ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
-    md.stage_enc(lds + kEncTab);
+    static_assert(Model::kTabE == EncLayout<kL>::kTab, "the model's tables where the layout puts them");
+    md.stage_enc(lds + EncLayout<kL>::kTab, kL);
     __syncthreads();
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kL + threadIdx.x;
     if (c >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));  // symbols per 16-B unit
     static_assert(U % SPP == 0 || SPP % U == 0, "points split units evenly");
-    constexpr int GU = 8;                                    // units per 128-B group
+    // units per group: 128 B (256 lanes), or 64 B for 1,024 lanes, whose 128 VGPRs cannot hold
+    // two 128-B groups of symbols and table ids beside the chain (the u8 encoder spilled)
+    constexpr int GU = kL == kLanes ? 8 : 4;
     constexpr int GS = GU * U;                               // symbols per group
     constexpr int TB = GS;                                   // table-id bytes per group
     const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
     const uint8_t* tsrc = Model::kTids ? tids + c * chunk_len : nullptr;
     uint8_t* dst = slots + c * slot_cap;
     const uint32_t npages_cap = static_cast<uint32_t>(slot_cap / 64);
-    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / 128);
+    const int ngroups = static_cast<int>(chunk_len * sizeof(Sym) / (16 * GU));
 
-    const MRing ring{4 * threadIdx.x};
+    const MRingT<kL> ring{4 * threadIdx.x};
     MPageOut pout;
-    EncLane e;
+    EncLaneT<kL> e;
     e.head = ini.head(c);  // Message::zeros() / random(seed + c)
-    e.f = MFunnel{0, 0, 0, ring.col, ring.col};
+    e.f = MFunnelT<kL>{0, 0, 0, ring.col, ring.col};
     e.err = 0;
     uint32_t fp = 0, over = 0;
     // page fp leaves once the position is a byte past it: a take-back never reaches a flushed page
@@ -349,7 +397,9 @@ __global__ __launch_bounds__(kLanes, 2) void k_menc(Model md, const Sym* __restr
 // whose pops can take more than four bytes (Uniform and LogUniform sizes up to 2^46).
 __device__ const uint4 kZeroPair[8] = {};  // the Zeros tail generator's bytes below a stream
 
-struct MChain {
+template <int kL>
+struct MChainT {
+    using Lay = DecLayout<kL>;
     const uint8_t* src;
     uint4 Q[8];
     int32_t low, P8, lim8;
@@ -357,21 +407,26 @@ struct MChain {
     uint64_t head;
     bool bad;  // a pushed-back byte that differs from the stream's: corrupt (ANS_E_MISMATCH)
 
+    // sixteen ring rows from one address: rows kL * 4 bytes = kL / 64 st64 units apart
     template <int R0>
     __device__ __forceinline__ uint32_t put_half(uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
-        const uint32_t base = col + R0 * kLanes * 4;
+        constexpr int st = kL / 64;
+        const uint32_t base = col + Lay::kRing + R0 * kL * 4;
         asm volatile(
-            "ds_write2st64_b32 %0, %1, %2 offset0:0 offset1:4\n\t"
-            "ds_write2st64_b32 %0, %3, %4 offset0:8 offset1:12\n\t"
-            "ds_write2st64_b32 %0, %5, %6 offset0:16 offset1:20\n\t"
-            "ds_write2st64_b32 %0, %7, %8 offset0:24 offset1:28\n\t"
-            "ds_write2st64_b32 %0, %9, %10 offset0:32 offset1:36\n\t"
-            "ds_write2st64_b32 %0, %11, %12 offset0:40 offset1:44\n\t"
-            "ds_write2st64_b32 %0, %13, %14 offset0:48 offset1:52\n\t"
-            "ds_write2st64_b32 %0, %15, %16 offset0:56 offset1:60"
+            "ds_write2st64_b32 %0, %1, %2 offset0:%17 offset1:%18\n\t"
+            "ds_write2st64_b32 %0, %3, %4 offset0:%19 offset1:%20\n\t"
+            "ds_write2st64_b32 %0, %5, %6 offset0:%21 offset1:%22\n\t"
+            "ds_write2st64_b32 %0, %7, %8 offset0:%23 offset1:%24\n\t"
+            "ds_write2st64_b32 %0, %9, %10 offset0:%25 offset1:%26\n\t"
+            "ds_write2st64_b32 %0, %11, %12 offset0:%27 offset1:%28\n\t"
+            "ds_write2st64_b32 %0, %13, %14 offset0:%29 offset1:%30\n\t"
+            "ds_write2st64_b32 %0, %15, %16 offset0:%31 offset1:%32"
             :
             : "v"(base), "v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
-              "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w)
+              "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w),
+              "i"(0), "i"(st), "i"(2 * st), "i"(3 * st), "i"(4 * st), "i"(5 * st), "i"(6 * st), "i"(7 * st),
+              "i"(8 * st), "i"(9 * st), "i"(10 * st), "i"(11 * st), "i"(12 * st), "i"(13 * st), "i"(14 * st),
+              "i"(15 * st)
             : "memory");
         return a0.x;
     }
@@ -380,7 +435,7 @@ struct MChain {
             put_half<16>(Q[4], Q[5], Q[6], Q[7]);
         } else {
             const uint32_t r0 = put_half<0>(Q[0], Q[1], Q[2], Q[3]);
-            *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(col + 32u * kLanes * 4)) = r0;  // mirror
+            *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(col + Lay::kRing + 32u * kL * 4)) = r0;  // mirror
         }
     }
     __device__ __forceinline__ void fetch_pair(int32_t m) {
@@ -408,12 +463,17 @@ struct MChain {
             Q[k] = make_uint4(ab(d[4 * k + 1], d[4 * k], b), ab(d[4 * k + 2], d[4 * k + 1], b),
                               ab(d[4 * k + 3], d[4 * k + 2], b), ab(d[4 * k + 4], d[4 * k + 3], b));
     }
+    // ring row (P8 >> 5) & 31 of the lane's column (the ring base added by the caller / offsets)
+    __device__ __forceinline__ uint32_t row_addr(int32_t p8) const {
+        uint32_t a;
+        asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(static_cast<uint32_t>(p8) & 0x3E0u), "i"(Lay::kRowShift - 5), "v"(col));
+        return a;
+    }
     // W = stream bytes [P, P+4): ring rows (P>>2)&31 and the next; P8 = 8P
     __device__ __forceinline__ void read_window() {
-        uint32_t a;
-        asm("v_lshl_or_b32 %0, %1, 5, %2" : "=v"(a) : "v"(static_cast<uint32_t>(P8) & 0x3E0u), "v"(col));
-        wy = lds_ld32(a);
-        wx = lds_ld32(a + 4 * kLanes);
+        const uint32_t a = row_addr(P8);
+        wy = lds_ld32(a + Lay::kRing);
+        wx = lds_ld32(a + Lay::kRing + 4 * kL);
     }
     __device__ __forceinline__ void form_window() { W = __builtin_amdgcn_alignbit(wx, wy, static_cast<uint32_t>(P8)); }
     __device__ __forceinline__ void start(const uint8_t* s, int32_t len) {
@@ -460,11 +520,14 @@ struct MChain {
     // head's low byte goes back onto the stream (P moves up one byte), where it must equal the
     // stream's own byte (checked against the ring; a mismatch is a corrupt stream).  Both rare
     // cases sit behind one 32-bit screen voted per wave.  Returns the bits the position moves down.
+    // kJ4 = false: no pop leaves the high word zero (every row's p K >= 2^32, ans_fast.hpp
+    // renorm_up8), so js = clz >> 3 needs no clamp
+    template <bool kJ4 = true>
     __device__ __forceinline__ int32_t renorm_up8(uint64_t L, uint32_t hL8) {
         const uint32_t h1 = hi32(head), h0 = lo32(head);
         uint32_t fb;
         asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
-        const uint32_t m = min(fb, 32u) & 0x38u;  // 8 js
+        const uint32_t m = kJ4 ? min(fb, 32u) & 0x38u : fb & 0x18u;  // 8 js
         const uint32_t sel = hi32(0x0706050403020100ull << m);
         const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
         head = mk64(xj1, xj0);
@@ -476,9 +539,7 @@ struct MChain {
                 m8 -= 8;
                 if (m == 0) {  // renorm_down: byte xj0 & 0xFF back onto the stream at P + 4
                     const int32_t p8 = P8 + 32;
-                    uint32_t a;
-                    asm("v_lshl_or_b32 %0, %1, 5, %2" : "=v"(a) : "v"(static_cast<uint32_t>(p8) & 0x3E0u), "v"(col));
-                    const uint32_t byte = (lds_ld32(a) >> (static_cast<uint32_t>(p8) & 31u)) & 0xFFu;
+                    const uint32_t byte = (lds_ld32(row_addr(p8) + Lay::kRing) >> (static_cast<uint32_t>(p8) & 31u)) & 0xFFu;
                     bad |= byte != (xj0 & 0xFFu);
                 }
             }
@@ -500,22 +561,28 @@ struct MChain {
     }
 };
 
+using MChain = MChainT<kLanes>;
+
 // The decode skeleton: chunk c's stream read from its end (Tail::pop, src/ans.rs:198-203),
 // unflatten (src/ans.rs:262-264), then IID / Independent::pop forward (src/codec.rs:393-399,
-// 422-424); the symbols leave in whole 128-B lines; at the end the message must be back at the
+// 422-424); the symbols leave in whole 128-B lines (64 B for 1,024 lanes); at the end the message must be back at the
 // chunk's initial one (src/ans.rs:56).  A point precedes every SPP symbols (at most 60 stream
 // bytes between points, so no window read reaches an unlanded page).
-template <class Model, typename Sym, int SPP>
-__global__ __launch_bounds__(kLanes, 2) void k_mdec(Model md, const uint8_t* __restrict__ slots, uint64_t slot_cap,
-                                                     const uint64_t* __restrict__ offsets,
-                                                     const uint32_t* __restrict__ lens,
-                                                     const uint8_t* __restrict__ tids, uint64_t chunk_len,
-                                                     uint64_t nfull, int gen_kind, Sym* __restrict__ out,
-                                                     uint32_t* __restrict__ status, ChunkInit ini) {
+// kL: the layout (DecLayout: 256 lanes, or 1,024 sharing one table image at LDS offset 0; the
+// model's tables must be built for it, Model::kTab).
+template <class Model, typename Sym, int SPP, int kL = kLanes>
+__global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_mdec(Model md, const uint8_t* __restrict__ slots,
+                                                                   uint64_t slot_cap,
+                                                                   const uint64_t* __restrict__ offsets,
+                                                                   const uint32_t* __restrict__ lens,
+                                                                   const uint8_t* __restrict__ tids, uint64_t chunk_len,
+                                                                   uint64_t nfull, int gen_kind, Sym* __restrict__ out,
+                                                                   uint32_t* __restrict__ status, ChunkInit ini) {
     extern __shared__ __align__(16) unsigned char lds[];
-    md.stage_dec(lds + kDecTab);
+    static_assert(Model::kTab == DecLayout<kL>::kTab, "the model's tables where the layout puts them");
+    md.stage_dec(lds + DecLayout<kL>::kTab, kL);
     __syncthreads();
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kL + threadIdx.x;
     if (c >= nfull) return;
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));
@@ -528,55 +595,62 @@ __global__ __launch_bounds__(kLanes, 2) void k_mdec(Model md, const uint8_t* __r
         atomicOr(status, 1u << ANS_E_LEN);
         return;
     }
-    MChain ch;
+    MChainT<kL> ch;
     ch.col = 4 * threadIdx.x;
     ch.start(slots + (offsets ? offsets[c] : c * slot_cap), static_cast<int32_t>(lens[c]));
     ch.pull_until(md.first_bound(tsrc));  // Message::unflatten: head 0, the first pop's renorm_up
     typename Model::DecState ds;
     md.dec_init(ds);
 
-    // the table ids of the unit being decoded and of the next (requested a unit ahead)
-    uint4 tcur = make_uint4(0, 0, 0, 0), tnext = make_uint4(0, 0, 0, 0);
-    if constexpr (Model::kTids) tcur = *reinterpret_cast<const uint4*>(tsrc);
-    uint4 q[8];
-    for (int u0 = 0; u0 < nunit; u0 += 8) {
+    // a line: LU units of output (128 B; 64 B for 1,024 lanes, whose 128 VGPRs cannot hold two
+    // 128-B id lines and an output line beside the chain: 40 VGPRs spilled)
+    constexpr int LU = kL == kLanes ? 8 : 4;
+    // the table ids of a line (LU * U bytes, one u32 word per four ids) and of the next line,
+    // whose load is issued at the line's first point: whole lines per load (r05: 16-B loads a
+    // unit apart left each lane's id line to be evicted between them, 5.3 GB read per launch for
+    // 2.1 GB of stream and ids at 2^30 u8 symbols)
+    constexpr int TW = LU * U / 4;  // u32 words of ids per line
+    uint32_t tl[TW], tn[TW];
+#pragma unroll
+    for (int k = 0; k < TW; ++k) tl[k] = tn[k] = 0;
+    auto load_ids = [&](int line, uint32_t* w) __attribute__((always_inline)) {
+        const uint4* g = reinterpret_cast<const uint4*>(tsrc + static_cast<int64_t>(LU) * U * line);
+#pragma unroll
+        for (int k = 0; k < TW / 4; ++k) {
+            const uint4 v = g[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+        }
+    };
+    if constexpr (Model::kTids) {
+        if (nunit > 0) load_ids(0, tl);
+    }
+    uint4 q[LU];
+    for (int u0 = 0; u0 < nunit; u0 += LU) {
         auto unit = [&](auto ic) __attribute__((always_inline)) {
             constexpr int uu = decltype(ic)::value;
-            const int u = u0 + uu;
             uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < U; ++j) {
                 if (j % SPP == 0) {
                     wait_vm();  // point
                     if (j == 0 && uu == 0 && u0 > 0) {
-                        uint4* d = dst + (u0 - 8);
+                        uint4* d = dst + (u0 - LU);
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) d[k] = q[k];
+                        for (int k = 0; k < LU; ++k) d[k] = q[k];
                     }
-                    if (j == 0 && Model::kTids) {
-                        if (uu > 0 || u0 > 0) tcur = tnext;
-                        if (u + 1 < nunit) {
-                            const int tb = (u + 1) * U;  // first table-id byte of the next unit
-                            tnext = make_uint4(0, 0, 0, 0);
-                            if constexpr (U == 16) tnext = *reinterpret_cast<const uint4*>(tsrc + tb);
-                            else if constexpr (U == 8) {
-                                const uint2 v = *reinterpret_cast<const uint2*>(tsrc + tb);
-                                tnext = make_uint4(v.x, v.y, 0, 0);
-                            } else if constexpr (U == 4) {
-                                tnext = make_uint4(*reinterpret_cast<const uint32_t*>(tsrc + tb), 0, 0, 0);
-                            } else {
-                                tnext = make_uint4(*reinterpret_cast<const uint16_t*>(tsrc + tb), 0, 0, 0);
-                            }
-                        }
+                    if constexpr (Model::kTids) {
+                        if (j == 0 && uu == 0 && u0 + LU < nunit) load_ids(u0 / LU + 1, tn);
                     }
                     ch.point();
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 uint32_t tid = 0;
                 if constexpr (Model::kTids) {
-                    const int wi = j / 4;
-                    const uint32_t w = wi == 0 ? tcur.x : wi == 1 ? tcur.y : wi == 2 ? tcur.z : tcur.w;
-                    tid = (w >> (8 * (j % 4))) & 0xFFu;
+                    const int tb = uu * U + j;  // id byte within the line (the pop fences the id)
+                    tid = (tl[tb / 4] >> (8 * (tb % 4))) & 0xFFu;
                 }
                 uint32_t hi = 0;
                 uint32_t lo = md.pop(ch, ds, tid, hi);
@@ -590,13 +664,17 @@ __global__ __launch_bounds__(kLanes, 2) void k_mdec(Model md, const uint8_t* __r
             asm volatile("" : "+v"(outv.x), "+v"(outv.y), "+v"(outv.z), "+v"(outv.w));
             q[uu] = outv;
         };
-        unroll_seq(unit, std::make_integer_sequence<int, 8>{});
+        unroll_seq(unit, std::make_integer_sequence<int, LU>{});
+        if constexpr (Model::kTids) {
+#pragma unroll
+            for (int k = 0; k < TW; ++k) tl[k] = tn[k];
+        }
     }
     wait_vm();
     if (nunit > 0) {  // the last line (nunit is a multiple of 8: chunk bytes % 128 == 0)
-        uint4* d = dst + (nunit - 8);
+        uint4* d = dst + (nunit - LU);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d[k] = q[k];
+        for (int k = 0; k < LU; ++k) d[k] = q[k];
     }
     // assert_eq!(initial, m) (src/ans.rs:56, 302-310)
     ch.pull_until(kMaxMinHead);
@@ -619,10 +697,11 @@ __device__ __forceinline__ uint64_t div_magic(uint64_t x, uint64_t d, uint64_t m
     return q;
 }
 
-// stage `bytes` (a multiple of 16) of a global image into LDS (every thread of the workgroup)
-__device__ __forceinline__ void stage_image(const uint4* __restrict__ g, uint32_t bytes, unsigned char* l) {
+// stage `bytes` (a multiple of 16) of a global image into LDS (every thread of a workgroup of nl)
+__device__ __forceinline__ void stage_image(const uint4* __restrict__ g, uint32_t bytes, unsigned char* l,
+                                            uint32_t nl = kLanes) {
     uint4* d = reinterpret_cast<uint4*>(l);
-    for (uint32_t i = threadIdx.x; i < bytes / 16; i += kLanes) d[i] = g[i];
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += nl) d[i] = g[i];
 }
 
 struct NoState {
@@ -633,10 +712,12 @@ struct NoState {
 // A set of T <= kIndMaxTables Categoricals with <= 256 symbols, all in one norm range (kNR)
 // (src/codec.rs:51-92), a table per position (src/codec.rs:366-403), table ids as one byte each.
 //
-// Encoder image (LDS kEncTab, the same bytes in global memory): row (t, s) at t*8224 + 32 s,
-// s < 257 (s >= nsym: zero mass), then K_t (u64) per table at k_off.  A row is
-//   {rcp = 1/p (f64), p, cdf(s), w, norm, screen}
-// read as two ds_read_b128.  w is the renorm word: every push starts from head in
+// Encoder image (LDS kTabE, the same bytes in global memory; r05: 24 B per row, so five 256-
+// symbol tables fit the 1,024-lane layout's 32 KiB): for row i = 257 t + s (s >= nsym: zero mass)
+// {p, cdf(s), w (u64)} at 16 i (one ds_read_b128: every 16-B read spans the LDS bank quads, where
+// 32-B rows used half of them), rcp = 1/p (f64) at ro + 8 i, norm_t (u32) at no + 4 t, K_t (u64)
+// at k_off + 8 t and, for sets with screened rows (kRare), screen (u32) at so + 4 i.  At most 15
+// tables (16 i below 2^16).  w is the renorm word: every push starts from head in
 // [Hmin, 2^64) (Hmin = min_t norm_t K_t > 2^56 - 2^31, or the chunk's initial head), where the
 // bounds pK 2^8j (src/ans.rs:246-253) below Hmin always count, and with T = the first above it,
 // k = k0 + [head >= T] whenever 2^8 T >= 2^64: w = T + 8 k0 (T's low byte is zero), one compare
@@ -653,39 +734,53 @@ struct NoState {
 // set when cdf(s0+3) still lies inside the bucket (a voted scan of the rows handles cf beyond
 // s0+2 there).  rshift = 32 - us >= 10 keeps the 9-bit symbol clear, so a table of norm 2^31
 // needs only 512 buckets.
-constexpr uint32_t kIndRowBytes = 32;
-constexpr uint32_t kIndTabStride = 257 * kIndRowBytes;  // 8224
-constexpr uint32_t kIndMaxTables = 31;                  // 32-B headers in 1 KiB, row offsets in 16 bits
+constexpr uint32_t kIndMaxTables = 15;                  // 16 (257 t + s) < 2^16; 32-B headers in 1 KiB
 constexpr uint32_t kIndRowOff = 1024;                   // decoder rows after the headers
 constexpr uint32_t kIndFarBit = 0x200u;
 constexpr uint32_t kIndMaxShift = 22;                   // rshift = 32 - us >= 10
 
 // kNR (ans_fast.hpp kNormStd / kNormSmall / kNormBig): every table of the set in that norm range;
 // kNormSmall rows carry 1/p rounded up and the headers 1/norm rounded up (the long division).
-template <bool kRare, int kNR = fast::kNormStd>
+// kTab: the LDS offset of the decoder image (DecLayout: kDecTab for 256-lane decoders, 0 for the
+// 1,024-lane one; the image's bucket addresses are built for it, IndepFast::dec_wide).
+// kLean (decoder): the image has no bucket with a third boundary (no far bits: the voted row
+// scan compiles out), every mass and hi32(q) is below 2^24 (the update's high word by one
+// v_mad_u32_u24, as ans_fast.hpp DecChain::update<kP24>) and every row's p K is at least 2^32
+// (kmax <= 3: the renorm's byte count needs no clamp).
+// kTabE: the LDS offset of the encoder image (EncLayout: kEncTab for 256-lane encoders, 0 for
+// the 1,024-lane one).
+template <bool kRare, int kNR = fast::kNormStd, uint32_t kTabD = kDecTab, bool kLean = false,
+          uint32_t kTabEnc = kEncTab>
 struct IndepModel {
     static constexpr bool kTids = true;
+    static constexpr uint32_t kTab = kTabD;
+    static constexpr uint32_t kTabE = kTabEnc;
     using DecState = NoState;
     const uint4* enc_img;
     const uint4* dec_img;
     const uint32_t* nsym;  // per table, global (error classification)
-    uint32_t enc_bytes, dec_bytes, k_off;
+    uint32_t enc_bytes, dec_bytes, k_off, ro, no, so;
 
-    __device__ __forceinline__ void stage_enc(unsigned char* l) const { stage_image(enc_img, enc_bytes, l); }
-    __device__ __forceinline__ void stage_dec(unsigned char* l) const { stage_image(dec_img, dec_bytes, l); }
+    __device__ __forceinline__ void stage_enc(unsigned char* l, uint32_t nl) const { stage_image(enc_img, enc_bytes, l, nl); }
+    __device__ __forceinline__ void stage_dec(unsigned char* l, uint32_t nl) const { stage_image(dec_img, dec_bytes, l, nl); }
 
     // blanket push (src/ans.rs:96-105) with Categorical t's row (src/codec.rs:63-64)
-    __device__ __forceinline__ void push(EncLane& e, uint32_t sym, uint32_t, uint32_t tid) const {
-        const uint32_t off = kEncTab + __umul24(tid, kIndTabStride) + (min(sym, 256u) << 5);
-        const uint4 ra = lds_ld128(off), rb = lds_ld128(off + 16);
-        const double rcp = __longlong_as_double(static_cast<long long>(mk64(ra.y, ra.x)));
-        const uint32_t mass = ra.z, cum = ra.w, norm = rb.z;
-        const uint64_t w = mk64(rb.y, rb.x);
-        uint32_t k8 = (rb.x & 0xFFu) + (mk64(hi32(e.head), lo32(e.head) | 0xFFu) > w ? 8u : 0u);
+    template <class E>
+    __device__ __forceinline__ void push(E& e, uint32_t sym, uint32_t, uint32_t tid) const {
+        const uint32_t i = __umul24(tid, 257u) + min(sym, 256u);  // row 257 t + s
+        const uint4 r = lds_ld128(kTabE + shl16<4>(i));          // {p, cdf, w}
+        uint32_t ra, na;
+        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(i), "s"(ro));
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(na) : "v"(tid), "s"(no));
+        const double rcp = __longlong_as_double(static_cast<long long>(lds_ld64(kTabE + ra)));
+        const uint32_t mass = r.x, cum = r.y, norm = lds_ld32(kTabE + na);
+        const uint64_t w = mk64(r.w, r.z);
+        uint32_t k8 = (r.z & 0xFFu) + (mk64(hi32(e.head), lo32(e.head) | 0xFFu) > w ? 8u : 0u);
         if constexpr (kRare) {
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(hi32(e.head) <= rb.w) != 0, 0)) {
-                if (hi32(e.head) <= rb.w) {  // exact renorm(pK): take back, then count (src/ans.rs:233-253)
-                    const uint64_t pK = static_cast<uint64_t>(mass) * lds_ld64(kEncTab + k_off + 8 * tid);
+            const uint32_t screen = lds_ld32(kTabE + so + 4 * i);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(hi32(e.head) <= screen) != 0, 0)) {
+                if (hi32(e.head) <= screen) {  // exact renorm(pK): take back, then count (src/ans.rs:233-253)
+                    const uint64_t pK = static_cast<uint64_t>(mass) * lds_ld64(kTabE + k_off + 8 * tid);
                     e.take_back_until(pK);
                     k8 = bytes_out8_exact(e.head, pK);
                 }
@@ -736,27 +831,28 @@ struct IndepModel {
     }
 
     __device__ __forceinline__ uint64_t first_bound(const uint8_t* t) const {
-        return lds_ld64(kDecTab + 32 * t[0] + 8);
+        return lds_ld64(kTab + 32 * t[0] + 8);
     }
     __device__ __forceinline__ void dec_init(DecState&) const {}
     __device__ __forceinline__ bool dec_bad(const DecState&) const { return false; }
     // blanket pop (src/ans.rs:107-116) with Categorical t's icdf (src/codec.rs:65-68)
-    __device__ __forceinline__ uint32_t pop(MChain& ch, DecState&, uint32_t tid, uint32_t& hi) const {
+    template <class Ch>
+    __device__ __forceinline__ uint32_t pop(Ch& ch, DecState&, uint32_t tid, uint32_t& hi) const {
         // (a volatile fence on the table id: the header reads of a unit's pops are not hoisted
         // ahead of the pops before them, which held every header in registers at once)
         asm volatile("" : "+v"(tid));
-        const uint32_t ha = kDecTab + shl16<5>(tid);
+        const uint32_t ha = kTab + shl16<5>(tid);
         const uint4 h0 = lds_ld128(ha), h1 = lds_ld128(ha + 16);
         const double rcp_norm = __longlong_as_double(static_cast<long long>(mk64(h0.y, h0.x)));
         const uint64_t L = mk64(h0.w, h0.z);
         const uint32_t norm = h1.x, hL8 = h1.y, bkt = h1.z;
-        const uint32_t us = h1.w & 0xFFu, rsh = (h1.w >> 8) & 0xFFu, rows = h1.w >> 16;  // rows: 8 * 257 t
+        const uint32_t us = h1.w & 0xFFu, rows = h1.w >> 16;  // rows: 8 * 257 t
         // the chain from the renorm to the bucket read at raised wave priority, as in the C3
         // decoder (ans_fast.hpp k_decode): decode -1.3% (profiles/r04h_ab_rejected.txt; a second
         // bracket around the row read gained nothing)
         __builtin_amdgcn_s_setprio(2);
         ch.form_window();
-        ch.P8 -= ch.renorm_up8(L, hL8);
+        ch.P8 -= ch.template renorm_up8<!kLean>(L, hL8);
         ch.read_window();  // for the next pop
         __builtin_amdgcn_sched_barrier(0);
         uint64_t qq;
@@ -764,7 +860,9 @@ struct IndepModel {
         fast::div_norm<kNR>(ch.head, norm, rcp_norm, qq, cf, -static_cast<double>(norm));
         const uint64_t cc = lds_ld64(bkt + ((cf >> us) << 3));
         __builtin_amdgcn_s_setprio(0);
-        const uint32_t rx = cf << rsh;
+        // rx = cf << (32 - us) as ({cf, 0} >> us): v_alignbit takes us from the header word's low
+        // five bits as they are (no unpacking of 32 - us)
+        const uint32_t rx = __builtin_amdgcn_alignbit(cf, 0u, h1.w);
         uint32_t sx;
         asm volatile(
             "v_cmp_gt_u32 vcc, %[rx], %[w1]\n\t"
@@ -777,17 +875,26 @@ struct IndepModel {
             : [rx] "v"(rx), [w1] "v"(lo32(cc)), [w2] "v"(hi32(cc))
             : "vcc");
         sx &= 0x1FFu;  // the symbol (w1's threshold bits above it dropped)
-        const bool far = (hi32(cc) & kIndFarBit) && rx > hi32(cc);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(far) != 0, 0)) {
-            if (far) {  // three or more boundaries in the bucket: scan the rows past s0 + 2
-                while (cf >= lo32(lds_ld64(kDecTab + kIndRowOff + rows + 8 * (sx + 1)))) ++sx;
+        if constexpr (!kLean) {
+            const bool far = (hi32(cc) & kIndFarBit) && rx > hi32(cc);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(far) != 0, 0)) {
+                if (far) {  // three or more boundaries in the bucket: scan the rows past s0 + 2
+                    while (cf >= lo32(lds_ld64(kTab + kIndRowOff + rows + 8 * (sx + 1)))) ++sx;
+                }
             }
         }
         uint32_t ra;
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(sx), "v"(rows));
-        const uint64_t row = lds_ld64(kDecTab + kIndRowOff + ra);  // (cdf(s), pmf(s))
+        const uint64_t row = lds_ld64(kTab + kIndRowOff + ra);  // (cdf(s), pmf(s))
         // head = pmf(s) q + cf - cdf(s) (src/ans.rs:113-114)
-        ch.head = qq * hi32(row) + (cf - lo32(row));
+        if constexpr (kLean) {
+            const uint64_t lo = static_cast<uint64_t>(lo32(qq)) * hi32(row) + (cf - lo32(row));
+            uint32_t h;
+            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(qq)), "v"(hi32(row)), "v"(hi32(lo)));
+            ch.head = mk64(h, lo32(lo));
+        } else {
+            ch.head = qq * hi32(row) + (cf - lo32(row));
+        }
         hi = 0;
         return sx;
     }
@@ -802,13 +909,16 @@ struct IndepModel {
 template <bool kPow2>
 struct UniformModel {
     static constexpr bool kTids = false;
+    static constexpr uint32_t kTab = kDecTab;
+    static constexpr uint32_t kTabE = kEncTab;
     using DecState = NoState;
     uint64_t size, K, L, w, magic;
     uint32_t log2size, hL8;
 
-    __device__ __forceinline__ void stage_enc(unsigned char*) const {}
-    __device__ __forceinline__ void stage_dec(unsigned char*) const {}
-    __device__ __forceinline__ void push(EncLane& e, uint32_t lo, uint32_t hi, uint32_t) const {
+    __device__ __forceinline__ void stage_enc(unsigned char*, uint32_t) const {}
+    __device__ __forceinline__ void stage_dec(unsigned char*, uint32_t) const {}
+    template <class E>
+    __device__ __forceinline__ void push(E& e, uint32_t lo, uint32_t hi, uint32_t) const {
         const uint64_t x = mk64(hi, lo);
         if (x >= size) e.err |= kErrSymbol;  // outside the alphabet (the reference would code garbage)
         const uint32_t k8 = (lo32(w) & 0xFFu) + (mk64(hi32(e.head), lo32(e.head) | 0xFFu) > w ? 8u : 0u);
@@ -820,7 +930,8 @@ struct UniformModel {
     __device__ __forceinline__ uint64_t first_bound(const uint8_t*) const { return L; }
     __device__ __forceinline__ void dec_init(DecState&) const {}
     __device__ __forceinline__ bool dec_bad(const DecState&) const { return false; }
-    __device__ __forceinline__ uint32_t pop(MChain& ch, DecState&, uint32_t, uint32_t& hi) const {
+    template <class Ch>
+    __device__ __forceinline__ uint32_t pop(Ch& ch, DecState&, uint32_t, uint32_t& hi) const {
         ch.renorm_wide(L, hL8);
         __builtin_amdgcn_sched_barrier(0);
         uint64_t x;
@@ -847,13 +958,16 @@ struct LogUniformState {
 };
 struct LogUniformModel {
     static constexpr bool kTids = false;
+    static constexpr uint32_t kTab = kDecTab;
+    static constexpr uint32_t kTabE = kEncTab;
     using DecState = LogUniformState;
     uint64_t nb, KE, LE, TEm1, magic;  // TEm1 = 2^8 KE - 1 (~0 when E = 0: no byte ever)
     uint32_t hL8E;
 
-    __device__ __forceinline__ void stage_enc(unsigned char*) const {}
-    __device__ __forceinline__ void stage_dec(unsigned char*) const {}
-    __device__ __forceinline__ void push(EncLane& e, uint32_t lo, uint32_t hi, uint32_t) const {
+    __device__ __forceinline__ void stage_enc(unsigned char*, uint32_t) const {}
+    __device__ __forceinline__ void stage_dec(unsigned char*, uint32_t) const {}
+    template <class E>
+    __device__ __forceinline__ void push(E& e, uint32_t lo, uint32_t hi, uint32_t) const {
         const uint64_t x = mk64(hi, lo);
         const uint32_t bits = x ? 64u - static_cast<uint32_t>(__builtin_clzll(x)) : 0u;  // LogUniform::get_bits
         if (bits >= nb) e.err |= kErrSymbol;                                               // assert!(bits < size)
@@ -878,7 +992,8 @@ struct LogUniformModel {
     __device__ __forceinline__ uint64_t first_bound(const uint8_t*) const { return LE; }
     __device__ __forceinline__ void dec_init(DecState& s) const { s.bad = false; }
     __device__ __forceinline__ bool dec_bad(const DecState& s) const { return s.bad; }
-    __device__ __forceinline__ uint32_t pop(MChain& ch, DecState& st, uint32_t, uint32_t& hi) const {
+    template <class Ch>
+    __device__ __forceinline__ uint32_t pop(Ch& ch, DecState& st, uint32_t, uint32_t& hi) const {
         ch.renorm_wide(LE, hL8E);
         __builtin_amdgcn_sched_barrier(0);
         uint64_t bits64;

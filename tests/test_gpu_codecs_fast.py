@@ -63,11 +63,15 @@ def _mixed_tables(rng):
     return t
 
 
+@pytest.mark.parametrize("lanes", [256, 1024])
 @pytest.mark.parametrize("dtype,L", [(np.uint8, 4096), (np.uint8, 128), (np.uint16, 1024), (np.uint32, 32)])
-def test_independent_fast_bit_exact(gpu, dtype, L):
+def test_independent_fast_bit_exact(gpu, dtype, L, lanes):
+    """Both kernel layouts (256-lane workgroups, or 1,024 sharing one LDS table image, which
+    calls of at least 1,024 chunks per CU take by default) code the same bytes."""
     rng = np.random.default_rng(L + np.dtype(dtype).itemsize)
     tables = _fast_tables(rng)
     ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
+    ts.lanes(lanes)
     assert ts.fast() == 1
     n = 37 * L + 29  # a ragged last chunk (exact kernel) after the fast chunks
     tids, syms = _indep_case(rng, tables, n)
@@ -114,6 +118,7 @@ def test_independent_fast_norm_ranges(gpu, which, dtype, L):
     for m in tables:
         assert (int(m.sum()) < 1 << 16) if which == "small" else ((1 << 31) < int(m.sum()) < (1 << 32))
     ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
+    ts.lanes(1024)  # (the big set's decoder buckets need more than 28 KiB: its encoder alone)
     assert ts.fast() in (1, 2)
     n = 301 * L + 17
     tids = rng.integers(0, len(tables), size=n).astype(np.uint32)

@@ -49,13 +49,17 @@ def line(n, sym_bytes, te, td, comp, **kw):
                 compressed_bytes_per_symbol=round(comp / n, 5), **kw)
 
 
-def device_case(gpu, codec, syms_np, L, w, tids_np=None):
-    stream = torch.cuda.Stream()
+def device_case(gpu, codec, syms_np, L, w, tids_np=None, stream=None):
+    """syms_np / tids_np: host arrays, or device tensors already in HBM (generated there)"""
+    stream = stream or torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     n = len(syms_np)
     nch = n // L
-    d_syms = torch.from_numpy(syms_np.view({1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[w])).cuda()
-    d_tids = None if tids_np is None else torch.from_numpy(tids_np.astype(np.uint8)).cuda()
+    if isinstance(syms_np, torch.Tensor):
+        d_syms, d_tids = syms_np, tids_np
+    else:
+        d_syms = torch.from_numpy(syms_np.view({1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[w])).cuda()
+        d_tids = None if tids_np is None else torch.from_numpy(tids_np.astype(np.uint8)).cuda()
     cap = codec.slot_capacity(L)
     slots = torch.empty(nch * cap, dtype=torch.uint8, device="cuda")
     lens = torch.zeros(nch, dtype=torch.int32, device="cuda")
@@ -98,22 +102,36 @@ def main():
     res = {"chunk_len": L, "kernels": "exact" if os.environ.get("ANS_CODECS_EXACT") == "1" else "fast",
            "what": "device-resident ans_dev_* encode + decode, HIP-event means of 10 passes; GiB/s of symbol bytes"}
 
-    # Independent: five 256-symbol tables (norm in the fast range), position k uses table k % 5
+    # Independent: five 256-symbol tables (norm in the fast range), position k uses table k % 5;
+    # the symbols of table t drawn on the device (its counter-based iid generator, seed t) and
+    # kept at the positions k = t mod 5
     n = 1 << li
     ms = [rng.integers(1, 1 << 16, 256).astype(np.uint64) for _ in range(5)]
     ts = A.GpuTableSet(g, [A.Categorical(m) for m in ms])
-    tids = (np.arange(n) % 5).astype(np.uint32)
-    syms = np.empty(n, np.uint8)
+    stream = torch.cuda.Stream()
+    d_tids = (torch.arange(n, device="cuda", dtype=torch.int64) % 5).to(torch.uint8)
+    d_syms = torch.empty(n, dtype=torch.uint8, device="cuda")
+    tmp = torch.empty(n, dtype=torch.uint8, device="cuda")
     for t in range(5):
-        p = ms[t].astype(np.float64)
-        sel = tids == t
-        syms[sel] = rng.choice(256, size=int(sel.sum()), p=p / p.sum())
-    te, td, comp = device_case(g, ts, syms, L, 1, tids)
+        A.GpuTable(g, A.Categorical(ms[t])).dev_gen_iid(t, 0, n, tmp, 1, stream)
+        torch.cuda.synchronize()
+        d_syms[t::5] = tmp[t::5]
+    del tmp
+    torch.cuda.synchronize()
+    te, td, comp = device_case(g, ts, d_syms, L, 1, d_tids, stream)
     res["independent"] = line(n, 1, te, td, comp, tables=5, table_symbols=256, tableset_fast=ts.fast())
+    if os.environ.get("CODECS_LANES_AB") == "1":  # both workgroup layouts, same box (ans_gpu_tableset_lanes)
+        for lanes in (256, 1024):
+            ts.lanes(lanes)
+            te, td, comp = device_case(g, ts, d_syms, L, 1, d_tids, stream)
+            res[f"independent_lanes{lanes}"] = line(n, 1, te, td, comp)
+        ts.lanes(0)
     if li <= 26:
+        tids, syms = d_tids.cpu().numpy().astype(np.uint32), d_syms.cpu().numpy()
         res["independent"].update(host_case(lambda: ts.encode_chunks(tids, syms, L),
                                             lambda e: ts.decode_chunks(tids, *e, L, np.uint8), n, 1))
-    del tids, syms
+    del d_tids, d_syms
+    torch.cuda.empty_cache()
 
     # Uniform(2^40) (a power of two: shifts) and Uniform(2^40 + 7) (the magic-reciprocal division)
     n = 1 << lu

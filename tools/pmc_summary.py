@@ -25,6 +25,11 @@ KEYS = ("k_encode_w", "k_encode", "k_decode_g", "k_decode_w", "k_decode", "k_gen
 
 def short(name):
     base = name.split("(")[0]
+    for key in ("k_menc", "k_mdec"):  # ans_mfast.hpp: one kernel per codec model
+        if key in base:
+            for model in ("IndepModel", "LogUniformModel", "UniformModel"):
+                if model in base:
+                    return f"mfast::{key}<{model}>"
     for key in KEYS:
         if key in base:
             return ("fast::" if "fast::" in base else "") + key
