@@ -580,13 +580,13 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
         uint4 ga = make_uint4(0, 0, 0, 0), gb = make_uint4(0, 0, 0, 0);
         if (!pre) {
             if constexpr (kCompact && !kPrefix) {  // the LDS copy of the first nlb buckets, else L2
+                // one load per lane into the same registers, L2 or LDS under complementary exec
+                // masks (r05: the LDS read on every lane and a 4-dword select added 12 VALU per
+                // symbol to the r04 decoder)
                 const uint32_t bi = cf >> cshift;
-                uint4 g = make_uint4(0, 0, 0, 0);
-                if (bi >= nlb) g = *reinterpret_cast<const uint4*>(bktc + bi);  // c0 | s0, d0 | d1, d2 | d3, d4
-                uint32_t la;
-                asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(la) : "v"(umin(bi, nlb - 1)), "s"(kWideDecTab));
-                const uint4 l = lds_ld128(la);
-                ga = bi < nlb ? l : g;
+                const uint4* gp = reinterpret_cast<const uint4*>(bktc + bi);  // c0 | s0, d0 | d1, d2 | d3, d4
+                const uint4* lp = reinterpret_cast<const uint4*>(lds + kWideDecTab) + bi;  // (generic: the LDS aperture)
+                ga = *(bi < nlb ? lp : gp);
             } else if constexpr (kCompact) {
                 ga = *reinterpret_cast<const uint4*>(bktc + (cf >> cshift));  // c0 | s0, d0 | d1, d2 | d3, d4
             } else {
