@@ -94,10 +94,16 @@ struct EncLayout {
     static constexpr uint32_t kTab = kL == kLanes ? kEncTab : 0u;
     static constexpr uint32_t kRowShift = kL == kLanes ? 10u : 12u;
     static constexpr uint32_t kRowMask = 31u << kRowShift;
+    static_assert(kL == kLanes || kRowShift == 12, "row_of's shift: (pos8 & 0x3E0) << 7");
     // the row address of stream bit position pos8 (dword pos8 >> 5), without the ring base
     static __device__ __forceinline__ uint32_t row_of(uint32_t pos8, uint32_t col) {
-        if constexpr (kL == kLanes) return (shl16<5>(pos8) & kRowMask) | col;  // (fits 16 bits)
-        else return ((pos8 << (kRowShift - 5)) & kRowMask) | col;
+        if constexpr (kL == kLanes) {
+            return (shl16<5>(pos8) & kRowMask) | col;  // (fits 16 bits)
+        } else {  // the mask first, then one v_lshl_or (ans_fast.hpp DecChain::read_window)
+            uint32_t a;
+            asm("v_lshl_or_b32 %0, %1, 7, %2" : "=v"(a) : "v"(pos8 & 0x3E0u), "v"(col));
+            return a;
+        }
     }
 };
 
@@ -280,8 +286,10 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, con
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));  // symbols per 16-B unit
     static_assert(U % SPP == 0 || SPP % U == 0, "points split units evenly");
     // units per group: 128 B (256 lanes), or 64 B for 1,024 lanes, whose 128 VGPRs cannot hold
-    // two 128-B groups of symbols and table ids beside the chain (the u8 encoder spilled)
-    constexpr int GU = kL == kLanes ? 8 : 4;
+    // two 128-B groups of symbols and table ids beside the chain (the u8 encoder spilled), and
+    // for u8 symbols without table ids (Uniform / LogUniform over 16 symbols a unit: the 128
+    // unrolled pushes of a 128-B group reached 256 VGPRs and spilled 76)
+    constexpr int GU = (kL == kLanes && (sizeof(Sym) > 1 || Model::kTids)) ? 8 : 4;
     constexpr int GS = GU * U;                               // symbols per group
     constexpr int TB = GS;                                   // table-id bytes per group
     const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
@@ -340,27 +348,40 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, con
                 // the symbol's words pass a volatile fence first, so that their unpacking stays
                 // at the push (hoisted to the group's start, the unpacked symbols of a whole
                 // group were held in registers and spilled)
-                uint4 cv = cc[u];
-                if constexpr (sizeof(Sym) == 8) {
-                    if (j == 0) asm volatile("" : "+v"(cv.x), "+v"(cv.y));
-                    else asm volatile("" : "+v"(cv.z), "+v"(cv.w));
-                } else {
-                    const int wi = j / (4 / static_cast<int>(sizeof(Sym)));  // (folded: j is unrolled)
-                    if (wi == 0) asm volatile("" : "+v"(cv.x));
-                    else if (wi == 1) asm volatile("" : "+v"(cv.y));
-                    else if (wi == 2) asm volatile("" : "+v"(cv.z));
-                    else asm volatile("" : "+v"(cv.w));
-                }
+                // (u8 / u16 symbols and the table ids: the field extract itself is the volatile
+                // asm, where an empty "+v" fence on the word made the compiler copy the word, which
+                // the later symbols of the unit still read: two v_mov per push, r05)
                 uint32_t lo, hi;
-                unit_sym<Sym>(cv, j, lo, hi);
+                if constexpr (sizeof(Sym) <= 2) {
+                    constexpr int per = 4 / static_cast<int>(sizeof(Sym));
+                    const int wi = j / per;  // (folded: j is unrolled)
+                    const uint32_t word = wi == 0 ? cc[u].x : wi == 1 ? cc[u].y : wi == 2 ? cc[u].z : cc[u].w;
+                    asm volatile("v_bfe_u32 %0, %1, %2, %3"
+                                 : "=v"(lo)
+                                 : "v"(word), "i"(8 * static_cast<int>(sizeof(Sym)) * (j % per)),
+                                   "i"(8 * static_cast<int>(sizeof(Sym))));
+                    hi = 0;
+                } else {
+                    uint4 cv = cc[u];
+                    if constexpr (sizeof(Sym) == 8) {
+                        if (j == 0) asm volatile("" : "+v"(cv.x), "+v"(cv.y));
+                        else asm volatile("" : "+v"(cv.z), "+v"(cv.w));
+                    } else {
+                        const int wi = j;  // (u32: a word per symbol)
+                        if (wi == 0) asm volatile("" : "+v"(cv.x));
+                        else if (wi == 1) asm volatile("" : "+v"(cv.y));
+                        else if (wi == 2) asm volatile("" : "+v"(cv.z));
+                        else asm volatile("" : "+v"(cv.w));
+                    }
+                    unit_sym<Sym>(cv, j, lo, hi);
+                }
                 uint32_t tid = 0;
                 if constexpr (Model::kTids) {
                     const int tb = u * U + j;  // table-id byte of this symbol within the group
                     const uint4& tv = tc[tb / 16];
                     const int wi = (tb % 16) / 4;
-                    uint32_t w = wi == 0 ? tv.x : wi == 1 ? tv.y : wi == 2 ? tv.z : tv.w;
-                    asm volatile("" : "+v"(w));
-                    tid = (w >> (8 * (tb % 4))) & 0xFFu;
+                    const uint32_t w = wi == 0 ? tv.x : wi == 1 ? tv.y : wi == 2 ? tv.z : tv.w;
+                    asm volatile("v_bfe_u32 %0, %1, %2, 8" : "=v"(tid) : "v"(w), "i"(8 * (tb % 4)));
                 }
                 md.push(e, lo, hi, tid);
             }
@@ -715,8 +736,9 @@ struct NoState {
 // Encoder image (LDS kTabE, the same bytes in global memory; r05: 24 B per row, so five 256-
 // symbol tables fit the 1,024-lane layout's 32 KiB): for row i = 257 t + s (s >= nsym: zero mass)
 // {p, cdf(s), w (u64)} at 16 i (one ds_read_b128: every 16-B read spans the LDS bank quads, where
-// 32-B rows used half of them), rcp = 1/p (f64) at ro + 8 i, norm_t (u32) at no + 4 t, K_t (u64)
-// at k_off + 8 t and, for sets with screened rows (kRare), screen (u32) at so + 4 i.  At most 15
+// 32-B rows used half of them), rcp = 1/p (f64) at ro + 8 i, {norm_t, -0x43300000 norm_t mod 2^32}
+// at no + 8 t, K_t (u64) at k_off + 8 t and, for sets with screened rows (kRare), screen (u32) at
+// so + 4 i.  At most 15
 // tables (16 i below 2^16).  w is the renorm word: every push starts from head in
 // [Hmin, 2^64) (Hmin = min_t norm_t K_t > 2^56 - 2^31, or the chunk's initial head), where the
 // bounds pK 2^8j (src/ans.rs:246-253) below Hmin always count, and with T = the first above it,
@@ -730,23 +752,22 @@ struct NoState {
 // norm, hL8 (the renorm screen), LDS address of bucket 0, us | rshift << 8 | 8*257*t << 16}, the
 // (cdf(s), pmf(s)) rows of every table at kIndRowOff + 8 (t*257 + s), then each table's icdf
 // buckets of width 2^us (ans_fast.hpp kModeU's folded words): bucket j at a = j << us holds
-// w1 = ((min(cdf(s0+1) - a, 2^us) - 1) << rshift) | s0 and w2 the same for cdf(s0+2) with bit 9
-// set when cdf(s0+3) still lies inside the bucket (a voted scan of the rows handles cf beyond
-// s0+2 there).  rshift = 32 - us >= 10 keeps the 9-bit symbol clear, so a table of norm 2^31
-// needs only 512 buckets.
+// w1 = ((min(cdf(s0+1) - a, 2^us) - 1) << rshift) | s0 and w2 the same for cdf(s0+2) (where
+// cdf(s0+3) still lies inside the bucket, cf beyond s0+2 shows as cf - cdf(s) >= pmf(s) on the
+// row and takes a voted scan of the rows).  rshift = 32 - us >= 10 keeps the 9-bit symbol clear,
+// so a table of norm 2^31 needs only 512 buckets.
 constexpr uint32_t kIndMaxTables = 15;                  // 16 (257 t + s) < 2^16; 32-B headers in 1 KiB
 constexpr uint32_t kIndRowOff = 1024;                   // decoder rows after the headers
-constexpr uint32_t kIndFarBit = 0x200u;
 constexpr uint32_t kIndMaxShift = 22;                   // rshift = 32 - us >= 10
 
 // kNR (ans_fast.hpp kNormStd / kNormSmall / kNormBig): every table of the set in that norm range;
 // kNormSmall rows carry 1/p rounded up and the headers 1/norm rounded up (the long division).
 // kTab: the LDS offset of the decoder image (DecLayout: kDecTab for 256-lane decoders, 0 for the
 // 1,024-lane one; the image's bucket addresses are built for it, IndepFast::dec_wide).
-// kLean (decoder): the image has no bucket with a third boundary (no far bits: the voted row
-// scan compiles out), every mass and hi32(q) is below 2^24 (the update's high word by one
-// v_mad_u32_u24, as ans_fast.hpp DecChain::update<kP24>) and every row's p K is at least 2^32
-// (kmax <= 3: the renorm's byte count needs no clamp).
+// kLean (decoder): every mass and hi32(q) is below 2^24 (the update's high word by one
+// v_mad_u32_u24, as ans_fast.hpp DecChain::update<kP24>), every row's p K is at least 2^32
+// (kmax <= 3: the renorm's byte count needs no clamp) and, in the standard range, every norm is
+// at least 2^20 (the quotient rounded to nearest with a voted fix-up, pop).
 // kTabE: the LDS offset of the encoder image (EncLayout: kEncTab for 256-lane encoders, 0 for
 // the 1,024-lane one).
 template <bool kRare, int kNR = fast::kNormStd, uint32_t kTabD = kDecTab, bool kLean = false,
@@ -771,9 +792,10 @@ struct IndepModel {
         const uint4 r = lds_ld128(kTabE + shl16<4>(i));          // {p, cdf, w}
         uint32_t ra, na;
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(i), "s"(ro));
-        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(na) : "v"(tid), "s"(no));
+        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(na) : "v"(tid), "s"(no));
         const double rcp = __longlong_as_double(static_cast<long long>(lds_ld64(kTabE + ra)));
-        const uint32_t mass = r.x, cum = r.y, norm = lds_ld32(kTabE + na);
+        const uint64_t nw = lds_ld64(kTabE + na);  // {norm, -0x43300000 norm}
+        const uint32_t mass = r.x, cum = r.y, norm = lo32(nw);
         const uint64_t w = mk64(r.w, r.z);
         uint32_t k8 = (r.z & 0xFFu) + (mk64(hi32(e.head), lo32(e.head) | 0xFFu) > w ? 8u : 0u);
         if constexpr (kRare) {
@@ -818,9 +840,17 @@ struct IndepModel {
             }
         }
         // head = norm * q + cdf(x, r) (src/ans.rs:103-104): q < 2^52, hi32(q) = the raw high word's
-        // low 20 bits (+ qh)
+        // low 20 bits (+ qh); outside kNormSmall the high word is one v_mul_lo_u32 of the raw word
+        // and a v_add3 with the table's -0x43300000 norm (r05: the mask and a 64-bit product took
+        // four VALU with their register moves)
         const uint64_t lo64 = static_cast<uint64_t>(lo32(qb)) * norm + (cum + rm);
-        e.head = mk64(hi32(lo64) + ((hi32(qb) & 0xFFFFFu) + qh) * norm, lo32(lo64));
+        if constexpr (kNR == fast::kNormSmall) {
+            e.head = mk64(hi32(lo64) + ((hi32(qb) & 0xFFFFFu) + qh) * norm, lo32(lo64));
+        } else {
+            uint32_t h;
+            asm("v_add3_u32 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(qb) * norm), "v"(hi32(lo64)), "v"(hi32(nw)));
+            e.head = mk64(h, lo32(lo64));
+        }
     }
     // a zero-mass lane: an out-of-range symbol (src/codec.rs:63) or p == 0 (src/ans.rs:98)
     template <typename Sym>
@@ -857,7 +887,33 @@ struct IndepModel {
         __builtin_amdgcn_sched_barrier(0);
         uint64_t qq;
         uint32_t cf;
-        fast::div_norm<kNR>(ch.head, norm, rcp_norm, qq, cf, -static_cast<double>(norm));
+        if constexpr (kNR == fast::kNormStd && kLean) {
+            // r05: q rounded to nearest in the 2^49 binade (the header holds 1/(8 norm), an exact
+            // scaling): t = fma(x, 1/(8 norm), 2^49 - 1/16) has raw bits 0x43000000'00000000 +
+            // round(x / norm - 1/2 + e), |e| < 2^-52 x / norm + 2^-48, which is q unless x / norm
+            // lies within |e| of an integer (kLean sets have every norm >= 2^20: x / norm < 2^44,
+            // |e| < 2^-8); cf = lo32(x) - lo32(q') norm is then outside [0, norm) and a voted branch
+            // moves q' by one.  The raw high word's low 24 bits are hi32(q), all the kLean update
+            // reads.  Replaces the estimate from below and its select-based fix-up (five VALU per
+            // pop) by one compare.
+            double hd;
+            asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(ch.head)));
+            const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(ch.head)));
+            double t;
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "v"(xd), "v"(rcp_norm), "v"(562949953421311.9375));
+            qq = static_cast<uint64_t>(__double_as_longlong(t));
+            cf = lo32(ch.head) - lo32(qq) * norm;
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(cf >= norm) != 0, 0)) {
+                if (cf >= norm) {  // q' = q +- 1: the remainder's sign in 64 bits (|r| < 2 norm)
+                    const int64_t r = static_cast<int64_t>(ch.head - (qq - 0x4300000000000000ull) * norm);
+                    const int64_t d = r < 0 ? -1 : 1;
+                    qq += static_cast<uint64_t>(d);
+                    cf = static_cast<uint32_t>(r - d * static_cast<int64_t>(norm));
+                }
+            }
+        } else {
+            fast::div_norm<kNR>(ch.head, norm, rcp_norm, qq, cf, -static_cast<double>(norm));
+        }
         const uint64_t cc = lds_ld64(bkt + ((cf >> us) << 3));
         __builtin_amdgcn_s_setprio(0);
         // rx = cf << (32 - us) as ({cf, 0} >> us): v_alignbit takes us from the header word's low
@@ -875,25 +931,30 @@ struct IndepModel {
             : [rx] "v"(rx), [w1] "v"(lo32(cc)), [w2] "v"(hi32(cc))
             : "vcc");
         sx &= 0x1FFu;  // the symbol (w1's threshold bits above it dropped)
-        if constexpr (!kLean) {
-            const bool far = (hi32(cc) & kIndFarBit) && rx > hi32(cc);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(far) != 0, 0)) {
-                if (far) {  // three or more boundaries in the bucket: scan the rows past s0 + 2
-                    while (cf >= lo32(lds_ld64(kTab + kIndRowOff + rows + 8 * (sx + 1)))) ++sx;
-                }
-            }
-        }
         uint32_t ra;
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(sx), "v"(rows));
         const uint64_t row = lds_ld64(kTab + kIndRowOff + ra);  // (cdf(s), pmf(s))
+        uint32_t p = hi32(row), r = cf - lo32(row);
+        // a bucket with three or more boundaries can leave cf past s0 + 2's interval: r >= pmf(s)
+        // is exactly that case (the thresholds never overshoot: cf >= cdf(sx)), one compare on the
+        // row the pop reads anyway (r05; the bucket's far bit and its test took five VALU), then a
+        // voted scan of the rows
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(r >= p) != 0, 0)) {
+            if (r >= p) {
+                while (cf >= lo32(lds_ld64(kTab + kIndRowOff + rows + 8 * (sx + 1)))) ++sx;
+                const uint64_t rw = lds_ld64(kTab + kIndRowOff + rows + 8 * sx);
+                p = hi32(rw);
+                r = cf - lo32(rw);
+            }
+        }
         // head = pmf(s) q + cf - cdf(s) (src/ans.rs:113-114)
         if constexpr (kLean) {
-            const uint64_t lo = static_cast<uint64_t>(lo32(qq)) * hi32(row) + (cf - lo32(row));
+            const uint64_t lo = static_cast<uint64_t>(lo32(qq)) * p + r;
             uint32_t h;
-            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(qq)), "v"(hi32(row)), "v"(hi32(lo)));
+            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(hi32(qq)), "v"(p), "v"(hi32(lo)));
             ch.head = mk64(h, lo32(lo));
         } else {
-            ch.head = qq * hi32(row) + (cf - lo32(row));
+            ch.head = qq * p + r;
         }
         hi = 0;
         return sx;

@@ -91,6 +91,44 @@ def test_independent_fast_mixed_norms(gpu, dtype, L):
         _check_indep(ts, tables, tids, syms, L, dtype, kind, seed)
 
 
+def _lean_edge_tables(rng):
+    """Lean sets (masses < 2^24, kmax <= 3) at the ends of the nearest-rounded quotient's range
+    (ans_mfast.hpp IndepModel::pop): norms just below 2^31, where q' = q - 1 and q' = q + 1 leave
+    overlapping 32-bit remainders (the voted fix-up decides in 64 bits), and norms of exactly 2^20,
+    where the estimate misses most often; crowded buckets (small masses) among them."""
+    big = rng.integers(1 << 23, 1 << 24, size=256).astype(np.uint64)
+    big = (big * ((1 << 31) - 7) // int(big.sum())).astype(np.uint64)
+    big[0] += np.uint64((1 << 31) - 7 - int(big.sum()))
+    crowd = np.concatenate([np.full(200, 64, np.int64), rng.integers(1 << 23, 1 << 24, size=56)])  # p K >= 2^32
+    t20 = np.maximum(1, rng.integers(1, 1 << 13, size=256) * (1 << 20) // (1 << 20))
+    t20 = np.maximum(1, t20 * (1 << 20) // int(t20.sum()))
+    t20[int(np.argmax(t20))] += (1 << 20) - int(t20.sum())
+    small20 = np.array([(1 << 20) - 5, 2, 3], np.uint64)
+    return [big, crowd.astype(np.uint64), t20.astype(np.uint64), small20]
+
+
+@pytest.mark.parametrize("lanes", [256, 1024])
+@pytest.mark.parametrize("dtype,L", [(np.uint8, 4096), (np.uint16, 512)])
+def test_independent_fast_lean_quotient_edges(gpu, dtype, L, lanes):
+    rng = np.random.default_rng(500 + L)
+    tables = _lean_edge_tables(rng)
+    for m in tables:
+        assert (1 << 20) <= int(m.sum()) < (1 << 31) and int(m.max()) < (1 << 24)
+    ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
+    ts.lanes(lanes)
+    assert ts.fast() == 1
+    n = 257 * L
+    tids = rng.integers(0, len(tables), size=n).astype(np.uint32)
+    syms = np.zeros(n, np.uint64)
+    for t, m in enumerate(tables):  # half uniform over the symbols (rare rows, crowded buckets)
+        sel = np.flatnonzero(tids == t)
+        p = m.astype(np.float64) / float(m.sum())
+        syms[sel] = np.where(rng.random(len(sel)) < 0.5, rng.choice(len(m), size=len(sel), p=p),
+                             rng.choice(np.flatnonzero(m), size=len(sel)))
+    for kind, seed in [(A.GEN_ZEROS, 0), (A.GEN_RANDOM, 6)]:
+        _check_indep(ts, tables, tids, syms, L, dtype, kind, seed)
+
+
 def _small_norm_tables(rng):
     """Count-built tables below 2^16 (src/benchmark.rs:549-578): a dataset edge Bernoulli, label
     counts with an absent label, Bernoulli::new(1, 2) (src/param_codec.rs:273), a 256-symbol one."""
