@@ -622,10 +622,14 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
             const uint32_t d0 = ga.y >> 16, d1 = ga.z & 0xFFFFu, d2 = ga.z >> 16, d3 = ga.w & 0xFFFFu,
                            d4 = ga.w >> 16;
             const bool b1 = rel >= d0, b2 = rel >= d1, b3 = rel >= d2, b4 = rel >= d3;
-            const uint32_t lo = b4 ? d3 : (b3 ? d2 : (b2 ? d1 : (b1 ? d0 : 0u)));
-            const uint32_t hi = b4 ? d4 : (b3 ? d3 : (b2 ? d2 : (b1 ? d1 : d0)));
-            p = hi - lo;
-            r = rel - lo;
+            // (lo, hi) = (d_{k-1}, d_k) as ONE packed word, selected among the five consecutive
+            // 16-bit pairs of the sequence 0, d0, .., d4 (two of them funnelled by v_alignbit):
+            // four selects where two chains of four selected lo and hi apart (r05)
+            const uint32_t w1 = __builtin_amdgcn_alignbit(ga.z, ga.y, 16u);  // d0 | d1
+            const uint32_t w3 = __builtin_amdgcn_alignbit(ga.w, ga.z, 16u);  // d2 | d3
+            const uint32_t pr = b4 ? ga.w : (b3 ? w3 : (b2 ? ga.z : (b1 ? w1 : (ga.y & 0xFFFF0000u))));
+            p = (pr >> 16) - (pr & 0xFFFFu);
+            r = rel - (pr & 0xFFFFu);
             sx = (ga.y & 0xFFFFu) + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
             far = rel >= d4;
         } else {
