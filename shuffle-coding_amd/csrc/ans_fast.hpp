@@ -984,13 +984,31 @@ struct DecChain {
         // and the magic 2^49 - 1/8 from a loop-invariant VGPR pair as the third operand of one
         // VOP3 v_fma_f64 (__builtin_fma became v_fmac_f64 on a v_mov_b64 copy of the magic: one
         // 64-bit move per step)
-        double hd;
-        asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
         uint32_t qh = 0;
-        if constexpr (kNR == kNormSmall) qh = div_hi(hd, rcp_norm, neg_norm);
-        const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
         double tq;
-        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(xd), "s"(rcp8), "v"(magic));
+        if constexpr (kNR == kNormStd) {
+            // r05: no conversion.  V = 2^64 + (head >> 12) 2^12 is a double by its bits alone:
+            // exponent field 0x43F and the 52-bit mantissa head >> 12, two v_alignbit where two
+            // v_cvt_f64_u32 and a v_fmac_f64 formed fl(head) (-1 VALU, -4.3 issue cycles per
+            // step).  magic here is (2^49 - 1/8) - 2^61 fl(1/norm) rounded once, so the fma takes
+            // the 2^64 back off with the same reciprocal: t = RN(V fl(1/(8 norm)) + magic) =
+            // 2^49 - 1/8 + x'/(8 norm) + e, x' in (head - 2^12, head], |e| < 2^-5 + 2^-8 (the
+            // magic's rounding in its binade below 2^49, the reciprocal's), so q_m stays in
+            // {q - 1, q} for every norm >= 2^16 (x' / norm is at most 2^-4 below head / norm;
+            // checked with exact rounding over 2.2e5 (head, norm) pairs, heads at multiples of the
+            // norm and 2^12 around them included)
+            uint32_t vlo, vhi;
+            asm("v_alignbit_b32 %0, %1, %2, 12" : "=v"(vlo) : "v"(hi32(head)), "v"(lo32(head)));
+            asm("v_alignbit_b32 %0, %1, %2, 12" : "=v"(vhi) : "s"(0x43Fu), "v"(hi32(head)));
+            const double vd = __longlong_as_double(static_cast<long long>(mk64(vhi, vlo)));
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(vd), "s"(rcp8), "v"(magic));
+        } else {
+            double hd;
+            asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"(hi32(head)));
+            if constexpr (kNR == kNormSmall) qh = div_hi(hd, rcp_norm, neg_norm);
+            const double xd = __builtin_fma(hd, 4294967296.0, static_cast<double>(lo32(head)));
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(tq) : "v"(xd), "s"(rcp8), "v"(magic));
+        }
         const uint64_t raw = static_cast<uint64_t>(__double_as_longlong(tq));  // q_m + 0x43000000'00000000
         cf = lo32(head) - lo32(raw) * norm;            // u (src/ans.rs:110-111 before the split)
         // (kNormSmall: + qh in the high word, q_m = qh 2^32 + the estimate)
@@ -1143,8 +1161,10 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const double rcp_norm = t.rcp_norm;  // (kNormSmall: rounded up)
     const double neg_norm = -static_cast<double>(norm);
     // 2^49 - 1/8 in a VGPR pair for the whole kernel (opaque, so it is not rematerialised per step)
+    // (kNormStd: less 2^61 fl(1/norm), rounded once: renorm_div_u's bit-built head)
     double magic_u;
-    asm("" : "=v"(magic_u) : "0"(562949953421311.875));
+    asm("" : "=v"(magic_u) : "0"(kNR == kNormStd ? 562949953421311.875 - 2305843009213693952.0 * rcp_norm
+                                                 : 562949953421311.875));
     const double rcp8 = rcp_norm * 0.125;
     const uint32_t shift = kMode == kModeU ? t.dec_u_shift : t.dec_shift;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
