@@ -387,7 +387,11 @@ struct PageOut {
 // (staged ragged / variable-length chunks, ans_kernels.hip launch_staged_encode); the pushes
 // past vlen[c], all in its first-coded group, are skipped.
 // kNR: the norm range (kNormStd / kNormSmall / kNormBig above; LDS rows only for the latter two).
-template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kVar = false, int kNR = kNormStd>
+// kM24 (LDS rows, kNormStd): every mass is below 2^24, so a row's mass word carries 8 k0 in its
+// top byte and its renorm word is T - 1: head >= T is then head > T - 1 on the head's own
+// register pair (r05; the (head | 0xFF) > T + 8 k0 form needed a v_or and a v_mov of the high
+// word into the pair beside it, two VALU per push, for one v_and of the mass)
+template <typename Sym, int KMAX, bool kK32, bool kGlobalRows, bool kVar = false, int kNR = kNormStd, bool kM24 = false>
 __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTable t, const Sym* __restrict__ syms,
                                                                          uint64_t chunk_len, uint64_t nfull,
                                                                          uint8_t* __restrict__ slots, uint64_t slot_cap,
@@ -396,6 +400,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                                                                          const uint32_t* __restrict__ vlen = nullptr) {
     static_assert(!(kVar && kGlobalRows), "staged chunks take the LDS-row kernel");
     static_assert(kNR == kNormStd || !kGlobalRows, "other norm ranges: LDS rows only");
+    static_assert(!kM24 || (!kGlobalRows && kNR == kNormStd), "kM24: the LDS rows of the standard range");
     extern __shared__ __align__(16) unsigned char lds[];
     // a symbol's row is two random LDS reads: rcp by ds_read_b64 (32-lane groups over 32 bank
     // pairs) and {mass, cum, renorm word} by one ds_read_b128 (16-lane groups over 16 bank
@@ -412,7 +417,12 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         for (uint32_t i = threadIdx.x; i < nrows; i += kBlock) {
             const EncRow r = i < t.enc_rows ? t.enc[i] : EncRow{0.0, 0u, 0u};
             const uint64_t w = enc_thr(static_cast<uint64_t>(r.mass) * t.K, t.L);
-            rows[i] = make_uint4(r.mass, r.cum, lo32(w), hi32(w));
+            if constexpr (kM24) {  // {mass | 8 k0 << 24, cum, T - 1} (T's low byte is zero)
+                const uint64_t tm1 = (w & ~0xFFull) - 1u;
+                rows[i] = make_uint4(r.mass | (lo32(w) << 24), r.cum, lo32(tm1), hi32(tm1));
+            } else {
+                rows[i] = make_uint4(r.mass, r.cum, lo32(w), hi32(w));
+            }
             rcps[i] = r.rcp;  // 0 for zero mass: such a push always takes the voted branch
         }
     }
@@ -472,6 +482,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     auto bytes_out_w8 = [&](uint64_t w) __attribute__((always_inline)) {
         const bool up = mk64(hi32(head), lo32(head) | 0xFFu) > w;
         return (lo32(w) & 0xFFu) + (up ? 8u : 0u);
+    };
+    // kM24: w = T - 1 and 8 k0 in the mass word's top byte
+    auto bytes_out_m24 = [&](uint64_t w, uint32_t mw) __attribute__((always_inline)) {
+        return (mw >> 24) + (head > w ? 8u : 0u);
     };
     // a zero-mass row (rcp 0: q_est 0, so rm = lo32(head) >= 0 = p) always takes the voted
     // branch, which records it (the reference's assert_ne!(p, 0), src/ans.rs:98)
@@ -545,7 +559,14 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
             // the push (the head chain) at raised wave priority, the row reads and page flushes
             // at the base one (encode -2.3% in a same-box A/B; the reads raised instead: +1.6%)
             __builtin_amdgcn_s_setprio(2);
-            push_one(e.e, bytes_out_w8(e.thr));
+            if constexpr (kM24) {
+                const uint32_t k8 = bytes_out_m24(e.thr, e.e.mass);
+                EncRow em = e.e;
+                em.mass &= 0xFFFFFFu;
+                push_one(em, k8);
+            } else {
+                push_one(e.e, bytes_out_w8(e.thr));
+            }
             __builtin_amdgcn_s_setprio(0);
         }
     };

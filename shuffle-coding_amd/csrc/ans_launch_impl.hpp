@@ -518,7 +518,9 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         const unsigned grid = static_cast<unsigned>((nfull + fast::kBlock - 1) / fast::kBlock);
         const size_t lds = fast::kEncSharedBytes;  // rows (LDS-row kernels) + ring
         const bool k32 = ft.K < (1ull << 32);
-#define ENC(KM, K32, G) fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+        const bool m24 = ft.pmax < (1u << 24);  // (k_encode kM24: the mass word's top byte is free)
+#define ENC(KM, K32, G) do { if (!(G) && m24) fast::k_encode<Sym, KM, K32, false, false, fast::kNormStd, true><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini); \
+                             else fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini); } while (0)
 #define ENCN(KM, K32, NR) fast::k_encode<Sym, KM, K32, false, false, NR><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
 #define ENC_KMAX(G)                                                   \
         if (!(G) && ft.nr == fast::kNormSmall) {                      \
