@@ -285,11 +285,16 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, con
 
     constexpr int U = 16 / static_cast<int>(sizeof(Sym));  // symbols per 16-B unit
     static_assert(U % SPP == 0 || SPP % U == 0, "points split units evenly");
-    // units per group: 128 B (256 lanes), or 64 B for 1,024 lanes, whose 128 VGPRs cannot hold
-    // two 128-B groups of symbols and table ids beside the chain (the u8 encoder spilled), and
-    // for u8 symbols without table ids (Uniform / LogUniform over 16 symbols a unit: the 128
-    // unrolled pushes of a 128-B group reached 256 VGPRs and spilled 76)
-    constexpr int GU = (kL == kLanes && (sizeof(Sym) > 1 || Model::kTids)) ? 8 : 4;
+    // units per group: 128 B, each group requested while the one before it is coded (kPre),
+    // except: 1,024 lanes (128 VGPRs) cannot hold two 128-B groups of symbols and table ids
+    // beside the chain (the u8 encoder spilled 190), so there a 128-B group is loaded at its own
+    // start, its latency covered by the SIMD's other three waves (r05: 64-B groups with the
+    // prefetch read 4.1 GB per launch for 2.15 GB of symbols and ids at 2^30 u8, each line's
+    // other half coming back from HBM after eviction); and u8 symbols without table ids
+    // (Uniform / LogUniform, 16 symbols a unit: the 128 unrolled pushes of a 128-B group reached
+    // 256 VGPRs and spilled 76) take 64-B groups
+    constexpr bool kPre = kL == kLanes;
+    constexpr int GU = (kL == kLanes && sizeof(Sym) == 1 && !Model::kTids) ? 4 : 8;
     constexpr int GS = GU * U;                               // symbols per group
     constexpr int TB = GS;                                   // table-id bytes per group
     const uint4* src = reinterpret_cast<const uint4*>(syms + c * chunk_len);
@@ -330,8 +335,9 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, con
             for (int i = 0; i < TB / 16; ++i) tn[i] = gt[i];
         }
     };
-    if (ngroups > 0) load_group(ngroups - 1);
+    if (kPre && ngroups > 0) load_group(ngroups - 1);
     for (int g = ngroups - 1; g >= 0; --g) {
+        if constexpr (!kPre) load_group(g);
         uint4 cc[GU], tc[GU];
 #pragma unroll
         for (int i = 0; i < GU; ++i) {
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, con
         }
         auto unit = [&](auto ic) __attribute__((always_inline)) {
             constexpr int u = GU - 1 - decltype(ic)::value;  // last unit first
-            if (u == GU / 2 - 1 && g > 0) load_group(g - 1);
+            if (kPre && u == GU / 2 - 1 && g > 0) load_group(g - 1);
 #pragma unroll
             for (int j = U - 1; j >= 0; --j) {  // last symbol first (src/codec.rs:417)
                 if ((j + 1) % SPP == 0 || j == U - 1) flush_ready();

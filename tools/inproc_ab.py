@@ -34,10 +34,84 @@ def load(d):
     return L
 
 
+def indep(dirs, iters, sync):
+    """AB_CONFIG=indep: tools/codecs_bench.py's Independent workload (five 256-symbol tables,
+    position k uses table k mod 5, 2^AB_LOG2N u8 symbols, default 30) on both builds."""
+    n, L = 1 << int(os.environ.get("AB_LOG2N", 30)), 4096
+    rng = np.random.default_rng(3)
+    ms = [rng.integers(1, 1 << 16, 256).astype(np.uint64) for _ in range(5)]
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    libs = [load(d) for d in dirs]
+    d_tids = (torch.arange(n, device="cuda", dtype=torch.int64) % 5).to(torch.uint8)
+    syms = torch.empty(n, dtype=torch.uint8, device="cuda")
+    setups = []
+    for i, Lb in enumerate(libs):
+        A._lib = Lb
+        gpu = A.Gpu(0)
+        if i == 0:
+            tmp = torch.empty(n, dtype=torch.uint8, device="cuda")
+            for t in range(5):
+                A.GpuTable(gpu, A.Categorical(ms[t])).dev_gen_iid(t, 0, n, tmp, 1, stream)
+                torch.cuda.synchronize()
+                syms[t::5] = tmp[t::5]
+            del tmp
+        ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in ms])
+        cap = ts.slot_capacity(L)
+        nch = n // L
+        setups.append(dict(ts=ts, cap=cap, slots=torch.empty(nch * cap, dtype=torch.uint8, device="cuda"),
+                           lens=torch.zeros(nch, dtype=torch.int32, device="cuda"),
+                           status=torch.zeros(1, dtype=torch.int32, device="cuda"), out=torch.empty_like(syms)))
+
+    def step(i, ev):
+        A._lib = libs[i]
+        s = setups[i]
+        ev[0].record(stream)
+        s["ts"].dev_encode(d_tids, syms, 1, n, L, s["slots"], s["cap"], s["lens"], s["status"], stream)
+        ev[1].record(stream)
+        s["ts"].dev_decode(d_tids, s["slots"], None, s["cap"], s["lens"], n, L, s["out"], 1, s["status"], stream)
+        ev[2].record(stream)
+
+    for _ in range(3):
+        for i in range(2):
+            step(i, [torch.cuda.Event(enable_timing=True) for _ in range(3)])
+    torch.cuda.synchronize()
+    evs = [[], []]
+    for it in range(iters):
+        for i in ((0, 1) if it % 2 == 0 else (1, 0)):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            step(i, ev)
+            evs[i].append(ev)
+        if sync:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for i in range(2):
+        s = setups[i]
+        A._lib = libs[i]
+        assert s["ts"].gpu.status(s["status"], stream) == 0
+        assert torch.equal(s["out"], syms), f"{dirs[i]}: round trip"
+        te = np.median([e[0].elapsed_time(e[1]) for e in evs[i]])
+        td = np.median([e[1].elapsed_time(e[2]) for e in evs[i]])
+        print(f"{dirs[i]:10s} enc {te:.4f} dec {td:.4f} ms (median of {iters})", flush=True)
+    # (the slots past each stream's length hold whatever the buffer held: compare the lengths
+    # and each stream's own bytes)
+    same = torch.equal(setups[0]["lens"], setups[1]["lens"])
+    if same:
+        cap = setups[0]["cap"]
+        lens = setups[0]["lens"].to(torch.int64)
+        pos = torch.arange(cap, device="cuda", dtype=torch.int64)
+        mask = (pos[None, :] < lens[:, None]).reshape(-1)
+        same = torch.equal(setups[0]["slots"][mask], setups[1]["slots"][mask])
+    print("streams: identical" if same else "note: the two builds' streams differ", flush=True)
+
+
 def main():
     dirs = sys.argv[1:3]
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     sync = os.environ.get("AB_NOSYNC") != "1"  # AB_NOSYNC=1: back-to-back launches, no idle gaps
+    if os.environ.get("AB_CONFIG") == "indep":
+        return indep(dirs, iters, sync)
     masses_name, log2n, sym_bytes, seed = bench.CONFIGS[os.environ.get("AB_CONFIG", "c3")]
     masses_fn = getattr(A, masses_name)
     dense = os.environ.get("AB_DENSE") == "1"
