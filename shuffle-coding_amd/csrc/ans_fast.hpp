@@ -707,7 +707,9 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
 // Returns 8k.  The permute selector (7-js, 6-js, 5-js, 4-js) is the high word of the byte ramp
 // 0x0706050403020100 shifted left by 8js: one 64-bit shift of the bit count 8js = clz & ~7,
 // where the byte count took a shift, a broadcasting v_perm and a subtract.
-template <bool kJ4 = true>
+// kScreen = false (k_decode's deferred screen): no test here; the caller takes max(hi32(head))
+// over a unit and re-runs the unit exactly when it reached the screen.
+template <bool kJ4 = true, bool kScreen = true>
 __device__ __forceinline__ uint32_t renorm_up8(uint64_t& head, uint32_t W, uint64_t L, uint32_t hL8) {
     const uint32_t h1 = hi32(head), h0 = lo32(head);
     uint32_t fb;
@@ -717,7 +719,7 @@ __device__ __forceinline__ uint32_t renorm_up8(uint64_t& head, uint32_t W, uint6
     const uint32_t xj1 = __builtin_amdgcn_perm(h1, h0, sel), xj0 = __builtin_amdgcn_perm(h0, W, sel);
     head = mk64(xj1, xj0);
     uint32_t m8 = m;
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(xj1 >= hL8) != 0, 0)) {
+    if (kScreen && __builtin_expect(__builtin_amdgcn_ballot_w64(xj1 >= hL8) != 0, 0)) {
         const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
         if (m != 0 && mk64(xm1, xm0) >= L) {
             head = mk64(xm1, xm0);
@@ -994,11 +996,11 @@ struct DecChain {
     // its low 24 bits ARE hi32(q_m), which is all that update<kP24>'s v_mad_u32_u24 reads, so the
     // v_and that cleared the exponent (0x433: bits 20-21 set) goes (kP24 only; decode -1 VALU per
     // symbol).  rcp8 = rcp_norm / 8 (exact).
-    template <bool kJ4, int kNR = kNormStd, bool kP24 = false>
+    template <bool kJ4, int kNR = kNormStd, bool kP24 = false, bool kScreen = true>
     __device__ __forceinline__ void renorm_div_u(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm, double rcp8,
                                                  double magic, double neg_norm = 0.0) {
         form_window();
-        P8 -= static_cast<int32_t>(renorm_up8<kJ4>(head, W, L, hL8));
+        P8 -= static_cast<int32_t>(renorm_up8<kJ4, kScreen>(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
         // 1/(8 norm) from its SGPR pair (an asm "v" operand copied it into a VGPR pair every step)
@@ -1178,6 +1180,8 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
     const uint32_t hL8 = renorm_screen(L);
     static_assert(!(kNR == kNormBig && kMode == kModeU), "u spans [0, 2 norm): 32 bits only below 2^31");
     static_assert(!(kNR == kNormSmall && kJ4), "norm < 2^16: p K >= 2^40, at most two bytes per pop");
+    // the deferred renorm screen (a unit re-run on the rare wave): one point per unit, u-domain
+    constexpr bool kDefer = kMode == kModeU && SPP == 16 / static_cast<int>(sizeof(Sym)) && !kVar;
     const uint32_t norm = t.norm;
     const double rcp_norm = t.rcp_norm;  // (kNormSmall: rounded up)
     const double neg_norm = -static_cast<double>(norm);
@@ -1216,6 +1220,27 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
             const int u = u0 + uu;
             if (u < nunit) {  // (uniform unless staged)
                 uint32_t sv[U];
+                // kDefer: the one-byte-less screen of the renorm (hi32(X) >= hL8, ~2^-24 of the
+                // steps) is taken once per unit as max(hi32(head)) over its steps instead of a
+                // compare per step; a wave where a lane reached it re-runs the unit from the
+                // head and position saved at the unit's point with the per-step screen (the ring
+                // is unchanged until the next point, and a step pulls at most KMAX bytes either
+                // way, so no read leaves the landed pages)
+                uint64_t h_pt = 0;
+                int32_t p_pt = 0;
+                uint32_t hmax = 0, hodd = 0;
+                static_assert(!kDefer || U % 2 == 0, "steps in pairs");
+                // (kPack4, u8 symbols: each four symbols' bytes packed into their output dword as
+                // soon as they are decoded, two v_perm and a v_or, so that the unit's sixteen
+                // symbols are not all live at its end beside the saved head: the deferred screen
+                // otherwise spilled)
+                constexpr bool kPack4 = kDefer && sizeof(Sym) == 1;
+                uint32_t pw[4] = {0, 0, 0, 0};
+                auto pack4 = [&](int k) __attribute__((always_inline)) {
+                    const uint32_t lo = __builtin_amdgcn_perm(sv[4 * k + 1], sv[4 * k], 0x0C0C0400u);
+                    const uint32_t hi = __builtin_amdgcn_perm(sv[4 * k + 3], sv[4 * k + 2], 0x04000C0Cu);
+                    pw[k] = lo | hi;
+                };
 #pragma unroll
                 for (int j = 0; j < U; ++j) {
                     sv[j] = 0;
@@ -1227,6 +1252,10 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                             for (int k = 0; k < 8; ++k) d[k] = q[k];
                         }
                         ch.point();
+                        if constexpr (kDefer) {
+                            h_pt = ch.head;
+                            p_pt = ch.P8;
+                        }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     if (kVar && static_cast<uint32_t>(u * U + j) >= nvalid) continue;  // past the chunk
@@ -1236,7 +1265,14 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                         // so the LDS round trip starts sooner (decode -6% in a same-box A/B,
                         // DESIGN.md §3.1)
                         __builtin_amdgcn_s_setprio(2);
-                        ch.template renorm_div_u<kJ4, kNR, kP24>(L, hL8, norm, rcp_norm, rcp8, magic_u, neg_norm);
+                        ch.template renorm_div_u<kJ4, kNR, kP24, !kDefer>(L, hL8, norm, rcp_norm, rcp8, magic_u, neg_norm);
+                        if constexpr (kDefer) {  // one v_max3 per two steps
+                            if (j % 2 == 0) {
+                                hodd = hi32(ch.head);
+                            } else {
+                                asm("v_max3_u32 %0, %1, %2, %3" : "=v"(hmax) : "v"(hmax), "v"(hodd), "v"(hi32(ch.head)));
+                            }
+                        }
                         ch.lookup_u(shift, 32u - shift);
                         __builtin_amdgcn_s_setprio(0);
                     } else {
@@ -1250,9 +1286,31 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                     }
                     ch.template update<kP24, kRows>();
                     sv[j] = ch.sx;  // kModeU: the virtual symbol (its low byte is the symbol)
+                    if constexpr (kPack4) {
+                        if (j % 4 == 3) pack4(j / 4);
+                    }
+                }
+                if constexpr (kDefer) {
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(hmax >= hL8) != 0, 0)) {
+                        ch.head = h_pt;  // the unit again, with the per-step screen
+                        ch.P8 = p_pt;
+                        ch.read_window();
+#pragma unroll
+                        for (int j = 0; j < U; ++j) {
+                            ch.template renorm_div_u<kJ4, kNR, kP24, true>(L, hL8, norm, rcp_norm, rcp8, magic_u, neg_norm);
+                            ch.lookup_u(shift, 32u - shift);
+                            ch.template update<kP24, kRows>();
+                            sv[j] = ch.sx;
+                            if constexpr (kPack4) {
+                                if (j % 4 == 3) pack4(j / 4);
+                            }
+                        }
+                    }
                 }
                 uint4 outv = make_uint4(0, 0, 0, 0);
-                if constexpr (sizeof(Sym) == 1 && kMode == kModeU) {  // the low bytes, by v_perm: two per dword and an or
+                if constexpr (kPack4) {
+                    outv = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+                } else if constexpr (sizeof(Sym) == 1 && kMode == kModeU) {  // the low bytes, by v_perm: two per dword and an or
                     uint32_t w[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {

@@ -992,3 +992,59 @@ def test_random_message_device_api(gpu):
     sl = slots.cpu().numpy()
     for c in (0, 1, 511, 1023):
         assert sl[c * cap: c * cap + lh[c]].tobytes() == od[int(oo[c]):int(oo[c]) + int(ol[c])].tobytes()
+
+
+def test_decoder_deferred_screen_reruns_the_unit(gpu):
+    """The C3 decoder takes the renorm's one-byte-less screen once per unit (ans_fast.hpp k_decode
+    kDefer) and re-runs a unit where a lane reached it.  Chunks whose first pop leaves the head at
+    exactly L (inside the window [L, 2^56) where the clz rule pulls one byte too many) force that
+    re-run; they sit in the same waves as ordinary chunks, and every chunk's symbols must equal
+    the oracle's pops of the same stream (the crafted streams end in a mismatch status, which
+    the ordinary ones must not share)."""
+    torch = pytest.importorskip("torch")
+    masses = A.c3_masses()
+    norm = int(masses.sum())
+    K = (1 << 56) // norm
+    L = norm * K
+    assert L < (1 << 56)
+    cum = np.concatenate([[0], np.cumsum(masses.astype(np.int64))])
+    big = [s for s in range(len(masses)) if int(masses[s]) * 250 > norm]  # H = q norm + cf < 2^64
+    chunk_len, nch = 4096, 512
+    rng = np.random.default_rng(77)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    cap = gt.slot_capacity(chunk_len)
+    slots = np.zeros(nch * cap, np.uint8)
+    lens = np.zeros(nch, np.uint32)
+    want = np.zeros(nch * chunk_len, np.uint32)
+    ocat = orc.Categorical(masses)
+    crafted = []
+    for c in range(nch):
+        if c % 3 == 1:  # crafted: H such that the first pop of symbol s leaves head = L
+            s = int(big[int(rng.integers(0, len(big)))])
+            q, rr = divmod(L, int(masses[s]))
+            H = norm * q + int(cum[s]) + rr
+            assert L <= H < (1 << 64)
+            data = orc.Message.unflatten(H.to_bytes(8, "little").rstrip(b"\0") or b"\0").flatten()
+            m1 = orc.Message.unflatten(data)
+            assert ocat.pop(m1) == s and m1.head == L  # the reference kept the head at L (no byte)
+            want[c * chunk_len:(c + 1) * chunk_len] = ocat.pop_iid(orc.Message.unflatten(data), chunk_len)
+            crafted.append(c)
+        else:  # an ordinary chunk
+            syms = orc.gen_iid(masses, 1000 + c, 0, chunk_len)
+            m = orc.Message.zeros()
+            ocat.push_iid(m, syms)
+            data = m.flatten()
+            want[c * chunk_len:(c + 1) * chunk_len] = syms
+        assert len(data) <= cap
+        slots[c * cap:c * cap + len(data)] = np.frombuffer(data, np.uint8)
+        lens[c] = len(data)
+    d_slots = torch.from_numpy(slots).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.zeros(nch * chunk_len, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    gt.dev_decode(d_slots, None, cap, d_lens, nch * chunk_len, chunk_len, out, 1, status)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for c in range(nch):
+        assert np.array_equal(got[c * chunk_len:(c + 1) * chunk_len], want[c * chunk_len:(c + 1) * chunk_len].astype(np.uint8)), c
+    assert int(status.item()) == 1 << A.ANS_E_MISMATCH  # the crafted streams do not return to their start
