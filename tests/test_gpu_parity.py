@@ -994,15 +994,26 @@ def test_random_message_device_api(gpu):
         assert sl[c * cap: c * cap + lh[c]].tobytes() == od[int(oo[c]):int(oo[c]) + int(ol[c])].tobytes()
 
 
-def test_decoder_deferred_screen_reruns_the_unit(gpu):
-    """The C3 decoder takes the renorm's one-byte-less screen once per unit (ans_fast.hpp k_decode
-    kDefer) and re-runs a unit where a lane reached it.  Chunks whose first pop leaves the head at
-    exactly L (inside the window [L, 2^56) where the clz rule pulls one byte too many) force that
-    re-run; they sit in the same waves as ordinary chunks, and every chunk's symbols must equal
-    the oracle's pops of the same stream (the crafted streams end in a mismatch status, which
-    the ordinary ones must not share)."""
+def _wide_rerun_masses():
+    """1,000 symbols (the wide decoder, ans_wide.hpp k_decode_w) with a few large masses."""
+    rng = np.random.default_rng(5)
+    m = rng.integers(1, 4097, 1000).astype(np.uint64)
+    m[[3, 500, 998]] = [1 << 22, 3 << 21, 1 << 21]
+    return m
+
+
+@pytest.mark.parametrize("which", ["c3_u8", "wide_u16"])
+def test_decoder_deferred_screen_reruns_the_unit(gpu, which):
+    """The C3 decoder takes the renorm's one-byte-less screen once per unit (ans_fast.hpp
+    k_decode kDefer) and re-runs a unit where a lane reached it; the large-alphabet decoder
+    (ans_wide.hpp k_decode_w) screens every step.  Chunks whose first pop leaves the head at
+    exactly L (inside the window [L, 2^56) where the clz rule pulls one byte too many) take
+    that path; they sit in the same waves as ordinary chunks, and every chunk's symbols must
+    equal the oracle's pops of the same stream (the crafted streams end in a mismatch status,
+    which the ordinary ones must not share)."""
     torch = pytest.importorskip("torch")
-    masses = A.c3_masses()
+    masses = A.c3_masses() if which == "c3_u8" else _wide_rerun_masses()
+    sym_bytes = 1 if which == "c3_u8" else 2
     norm = int(masses.sum())
     K = (1 << 56) // norm
     L = norm * K
@@ -1012,6 +1023,7 @@ def test_decoder_deferred_screen_reruns_the_unit(gpu):
     chunk_len, nch = 4096, 512
     rng = np.random.default_rng(77)
     gt = A.GpuTable(gpu, A.Categorical(masses))
+    assert gt.decode_kernel(sym_bytes) == ("lds" if which == "c3_u8" else "wide")
     cap = gt.slot_capacity(chunk_len)
     slots = np.zeros(nch * cap, np.uint8)
     lens = np.zeros(nch, np.uint32)
@@ -1040,11 +1052,12 @@ def test_decoder_deferred_screen_reruns_the_unit(gpu):
         lens[c] = len(data)
     d_slots = torch.from_numpy(slots).cuda()
     d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
-    out = torch.zeros(nch * chunk_len, dtype=torch.uint8, device="cuda")
+    dt = np.uint8 if sym_bytes == 1 else np.uint16
+    out = torch.zeros(nch * chunk_len, dtype=torch.uint8 if sym_bytes == 1 else torch.int16, device="cuda")
     status = torch.zeros(1, dtype=torch.int32, device="cuda")
-    gt.dev_decode(d_slots, None, cap, d_lens, nch * chunk_len, chunk_len, out, 1, status)
+    gt.dev_decode(d_slots, None, cap, d_lens, nch * chunk_len, chunk_len, out, sym_bytes, status)
     torch.cuda.synchronize()
-    got = out.cpu().numpy()
+    got = out.cpu().numpy().view(dt)
     for c in range(nch):
-        assert np.array_equal(got[c * chunk_len:(c + 1) * chunk_len], want[c * chunk_len:(c + 1) * chunk_len].astype(np.uint8)), c
+        assert np.array_equal(got[c * chunk_len:(c + 1) * chunk_len], want[c * chunk_len:(c + 1) * chunk_len].astype(dt)), c
     assert int(status.item()) == 1 << A.ANS_E_MISMATCH  # the crafted streams do not return to their start
