@@ -549,8 +549,12 @@ struct MChainT {
     // cases sit behind one 32-bit screen voted per wave.  Returns the bits the position moves down.
     // kJ4 = false: no pop leaves the high word zero (every row's p K >= 2^32, ans_fast.hpp
     // renorm_up8), so js = clz >> 3 needs no clamp
-    template <bool kJ4 = true>
-    __device__ __forceinline__ int32_t renorm_up8(uint64_t L, uint32_t hL8) {
+    static __device__ __forceinline__ uint64_t l_of(uint64_t L) { return L; }
+    template <class F>
+    static __device__ __forceinline__ uint64_t l_of(const F& f) { return f(); }
+    // (L: the bound, or a callable that reads it: only the rare path needs it)
+    template <bool kJ4 = true, class LT = uint64_t>
+    __device__ __forceinline__ int32_t renorm_up8(const LT& L, uint32_t hL8) {
         const uint32_t h1 = hi32(head), h0 = lo32(head);
         uint32_t fb;
         asm("v_ffbh_u32 %0, %1" : "=v"(fb) : "v"(h1));
@@ -561,7 +565,7 @@ struct MChainT {
         int32_t m8 = static_cast<int32_t>(m);
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(xj1 >= hL8) != 0, 0)) {
             const uint32_t xm1 = xj1 >> 8, xm0 = ab(xj1, xj0, 1);
-            if (xj1 >= hL8 && mk64(xm1, xm0) >= L) {
+            if (xj1 >= hL8 && mk64(xm1, xm0) >= l_of(L)) {
                 head = mk64(xm1, xm0);
                 m8 -= 8;
                 if (m == 0) {  // renorm_down: byte xj0 & 0xFF back onto the stream at P + 4
@@ -754,16 +758,26 @@ struct NoState {
 // a screen: hi32(head) <= screen sends the lane to the exact renorm on a voted branch (kRare;
 // sets without such rows compile it out).
 //
-// Decoder image (LDS kDecTab): a 32-B header per table at t*32 {1/norm (f64), L = norm K (u64),
-// norm, hL8 (the renorm screen), LDS address of bucket 0, us | rshift << 8 | 8*257*t << 16}, the
-// (cdf(s), pmf(s)) rows of every table at kIndRowOff + 8 (t*257 + s), then each table's icdf
+// Decoder image (LDS kDecTab): a 16-B header per table at 16 t {1/norm (f64; lean standard-range
+// sets 1/(8 norm)), norm, us | (bucket 0's offset / 8) << 5 | 257 t << 19}, L = norm K (u64) at
+// kIndLOff + 8 t (read only by the renorm's rare path and the unflatten), the renorm screen the
+// constant 0xFFFFFF00 for every table (r05: one ds_read_b128 per pop where a 32-B header took
+// two; the decoder is LDS-bound), the (cdf(s), pmf(s)) rows of every table at
+// kIndRowOff + 8 (t*257 + s), then each table's icdf
 // buckets of width 2^us (ans_fast.hpp kModeU's folded words): bucket j at a = j << us holds
 // w1 = ((min(cdf(s0+1) - a, 2^us) - 1) << rshift) | s0 and w2 the same for cdf(s0+2) (where
 // cdf(s0+3) still lies inside the bucket, cf beyond s0+2 shows as cf - cdf(s) >= pmf(s) on the
 // row and takes a voted scan of the rows).  rshift = 32 - us >= 10 keeps the 9-bit symbol clear,
 // so a table of norm 2^31 needs only 512 buckets.
-constexpr uint32_t kIndMaxTables = 15;                  // 16 (257 t + s) < 2^16; 32-B headers in 1 KiB
+constexpr uint32_t kIndMaxTables = 15;                  // 16 (257 t + s) < 2^16
+constexpr uint32_t kIndHdrBytes = 16;                   // decoder header per table at kIndHdrBytes t
+constexpr uint32_t kIndLOff = 256;                      // L_t at kIndLOff + 8 t (the renorm's rare path)
 constexpr uint32_t kIndRowOff = 1024;                   // decoder rows after the headers
+constexpr uint32_t kIndBktShift = 5;                    // header word: us | bucket offset / 8 << 5 | 257 t << 19
+constexpr uint32_t kIndRowShift = 19;
+static_assert(kIndHdrBytes * kIndMaxTables <= kIndLOff && kIndLOff + 8 * kIndMaxTables <= kIndRowOff, "header area");
+static_assert(257 * (kIndMaxTables - 1) < (1u << (32 - kIndRowShift)), "row index field");
+constexpr uint32_t kScreenAll = 0xFFFFFF00u;  // hi32(L) << 8 >= this for every norm < 2^32 (L > 2^56 - 2^32)
 constexpr uint32_t kIndMaxShift = 22;                   // rshift = 32 - us >= 10
 
 // kNR (ans_fast.hpp kNormStd / kNormSmall / kNormBig): every table of the set in that norm range;
@@ -867,7 +881,7 @@ struct IndepModel {
     }
 
     __device__ __forceinline__ uint64_t first_bound(const uint8_t* t) const {
-        return lds_ld64(kTab + 32 * t[0] + 8);
+        return lds_ld64(kTab + kIndLOff + 8 * t[0]);
     }
     __device__ __forceinline__ void dec_init(DecState&) const {}
     __device__ __forceinline__ bool dec_bad(const DecState&) const { return false; }
@@ -877,18 +891,16 @@ struct IndepModel {
         // (a volatile fence on the table id: the header reads of a unit's pops are not hoisted
         // ahead of the pops before them, which held every header in registers at once)
         asm volatile("" : "+v"(tid));
-        const uint32_t ha = kTab + shl16<5>(tid);
-        const uint4 h0 = lds_ld128(ha), h1 = lds_ld128(ha + 16);
-        const double rcp_norm = __longlong_as_double(static_cast<long long>(mk64(h0.y, h0.x)));
-        const uint64_t L = mk64(h0.w, h0.z);
-        const uint32_t norm = h1.x, hL8 = h1.y, bkt = h1.z;
-        const uint32_t us = h1.w & 0xFFu, rows = h1.w >> 16;  // rows: 8 * 257 t
+        const uint4 h = lds_ld128(kTab + shl16<4>(tid));
+        const double rcp_norm = __longlong_as_double(static_cast<long long>(mk64(h.y, h.x)));
+        const uint32_t norm = h.z, hw = h.w;  // hw: us | bkt / 8 << 5 | 257 t << 19
+        const auto L = [&]() __attribute__((always_inline)) { return lds_ld64(kTab + kIndLOff + 8 * tid); };
         // the chain from the renorm to the bucket read at raised wave priority, as in the C3
         // decoder (ans_fast.hpp k_decode): decode -1.3% (profiles/r04h_ab_rejected.txt; a second
         // bracket around the row read gained nothing)
         __builtin_amdgcn_s_setprio(2);
         ch.form_window();
-        ch.P8 -= ch.template renorm_up8<!kLean>(L, hL8);
+        ch.P8 -= ch.template renorm_up8<!kLean>(L, kScreenAll);
         ch.read_window();  // for the next pop
         __builtin_amdgcn_sched_barrier(0);
         uint64_t qq;
@@ -920,11 +932,15 @@ struct IndepModel {
         } else {
             fast::div_norm<kNR>(ch.head, norm, rcp_norm, qq, cf, -static_cast<double>(norm));
         }
-        const uint64_t cc = lds_ld64(bkt + ((cf >> us) << 3));
+        // the bucket at kTab + ((cf >> us) + bkt / 8) * 8 (v_lshrrev takes us from the word's low
+        // five bits; v_bfe the offset; one v_add_lshl)
+        uint32_t ba;
+        asm("v_add_lshl_u32 %0, %1, %2, 3" : "=v"(ba) : "v"(cf >> hw), "v"(__builtin_amdgcn_ubfe(hw, kIndBktShift, kIndRowShift - kIndBktShift)));
+        const uint64_t cc = lds_ld64(kTab + ba);
         __builtin_amdgcn_s_setprio(0);
         // rx = cf << (32 - us) as ({cf, 0} >> us): v_alignbit takes us from the header word's low
         // five bits as they are (no unpacking of 32 - us)
-        const uint32_t rx = __builtin_amdgcn_alignbit(cf, 0u, h1.w);
+        const uint32_t rx = __builtin_amdgcn_alignbit(cf, 0u, hw);
         uint32_t sx;
         asm volatile(
             "v_cmp_gt_u32 vcc, %[rx], %[w1]\n\t"
@@ -937,8 +953,9 @@ struct IndepModel {
             : [rx] "v"(rx), [w1] "v"(lo32(cc)), [w2] "v"(hi32(cc))
             : "vcc");
         sx &= 0x1FFu;  // the symbol (w1's threshold bits above it dropped)
+        const uint32_t r257 = hw >> kIndRowShift;  // 257 t: the table's first row
         uint32_t ra;
-        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(sx), "v"(rows));
+        asm("v_add_lshl_u32 %0, %1, %2, 3" : "=v"(ra) : "v"(sx), "v"(r257));
         const uint64_t row = lds_ld64(kTab + kIndRowOff + ra);  // (cdf(s), pmf(s))
         uint32_t p = hi32(row), r = cf - lo32(row);
         // a bucket with three or more boundaries can leave cf past s0 + 2's interval: r >= pmf(s)
@@ -947,8 +964,8 @@ struct IndepModel {
         // voted scan of the rows
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(r >= p) != 0, 0)) {
             if (r >= p) {
-                while (cf >= lo32(lds_ld64(kTab + kIndRowOff + rows + 8 * (sx + 1)))) ++sx;
-                const uint64_t rw = lds_ld64(kTab + kIndRowOff + rows + 8 * sx);
+                while (cf >= lo32(lds_ld64(kTab + kIndRowOff + 8 * (r257 + sx + 1)))) ++sx;
+                const uint64_t rw = lds_ld64(kTab + kIndRowOff + 8 * (r257 + sx));
                 p = hi32(rw);
                 r = cf - lo32(rw);
             }
