@@ -323,6 +323,18 @@ int ans_gpu_independent_encode_chunks(ans_gpu_tableset *ts, const uint32_t *tabl
 int ans_gpu_independent_decode_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const uint8_t *in,
                                       uint64_t in_len, const uint64_t *offsets, const uint64_t *lens, uint64_t n,
                                       uint64_t chunk_len, int gen_kind, uint64_t seed, void *out, int sym_bytes);
+/* Independent<Categorical> over variable-length chunks: chunk c is positions [starts[c], starts[c+1])
+ * (nchunks + 1 non-decreasing entries; table_ids / syms / out span [0, starts[nchunks])), one
+ * reference message each, e.g. one record of mixed fields per chunk.  These run on the exact
+ * 64-bit kernels (one lane per chunk), which take any chunk length. */
+int ans_gpu_independent_encode_var_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const void *syms,
+                                          int sym_bytes, uint64_t nchunks, const uint64_t *starts, int gen_kind,
+                                          uint64_t seed, uint8_t *out, uint64_t out_cap, uint64_t *offsets,
+                                          uint64_t *lens, uint64_t *total);
+int ans_gpu_independent_decode_var_chunks(ans_gpu_tableset *ts, const uint32_t *table_ids, const uint8_t *in,
+                                          uint64_t in_len, const uint64_t *offsets, const uint64_t *lens,
+                                          uint64_t nchunks, const uint64_t *starts, int gen_kind, uint64_t seed,
+                                          void *out, int sym_bytes);
 /* 1 (fast kernels: every table has <= 256 symbols, the norms all in [2^16, 2^31], all below
  * 2^16 or all in (2^31, 2^32), and at most 15 tables: 257 encoder rows of 32 B per table beside
  * the 32-KiB stream ring in 160 KiB of LDS), 2 (the same, with rows of near-certain symbols that
@@ -369,6 +381,16 @@ int ans_dev_independent_decode(ans_gpu_tableset *ts, const uint8_t *d_tids, cons
                                const uint64_t *d_offsets, uint64_t slot_cap, const uint32_t *d_lens, uint64_t n,
                                uint64_t chunk_len, int gen_kind, uint64_t seed, void *d_syms, int sym_bytes,
                                uint32_t *d_status, void *stream);
+/* ... over variable-length chunks (d_starts: nchunks + 1 device entries; slot_cap from
+ * ans_gpu_tableset_slot_capacity of the longest chunk; d_tids one byte per position) */
+int ans_dev_independent_encode_var(ans_gpu_tableset *ts, const uint8_t *d_tids, const void *d_syms, int sym_bytes,
+                                   uint64_t nchunks, const uint64_t *d_starts, int gen_kind, uint64_t seed,
+                                   uint8_t *d_slots, uint64_t slot_cap, uint32_t *d_lens, uint32_t *d_status,
+                                   void *stream);
+int ans_dev_independent_decode_var(ans_gpu_tableset *ts, const uint8_t *d_tids, const uint8_t *d_in,
+                                   const uint64_t *d_offsets, uint64_t slot_cap, const uint32_t *d_lens,
+                                   uint64_t nchunks, const uint64_t *d_starts, int gen_kind, uint64_t seed,
+                                   void *d_syms, int sym_bytes, uint32_t *d_status, void *stream);
 
 /* ======================================================================
  * (5) Graph models' bulk-IID caller — DenseSetIID<EdgeIndex, AllEdgeIndices> with an
@@ -412,6 +434,41 @@ int ans_gpu_dense_sets_encode(ans_gpu_table *gt, uint64_t num_graphs, const uint
 int ans_gpu_dense_sets_decode(ans_gpu_table *gt, uint64_t num_graphs, const uint32_t *num_nodes, int directed,
                               int loops, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
                               const uint64_t *lens, uint32_t *edges, uint64_t cap, uint64_t *edge_offsets);
+
+/* ======================================================================
+ * (5b) GraphIID<NodeC, EdgeC, ErdosRenyi> over a dataset (src/graph_codec.rs:19-94), the model
+ *      the reference's --er runs on node- and edge-labelled datasets: Independent of one
+ *      GraphIID per graph (src/benchmark.rs:308-316, 349-358) with count-built Categorical labels
+ *      (DatasetStats::node_label_dist / edge_label_dist, src/benchmark.rs:568-578) or, for
+ *      --uniform-er, Uniform(size) labels (src/benchmark.rs:318-330, 360-372: pass the all-ones
+ *      Categorical of that size, whose arithmetic is Uniform's: pmf 1, cdf x, norm size).
+ *      Tables come from one table set: node_table and edge_table index it (ANS_NO_TABLE =
+ *      EmptyCodec, nothing coded), edge_indicator_table is the Bernoulli (two symbols).  Graph g
+ *      (num_nodes[g] nodes, node labels [sum of earlier num_nodes, + num_nodes[g]) of node_labels,
+ *      edges [edge_offsets[g], edge_offsets[g+1]) of edges / edge_labels) is ONE message:
+ *      Message::zeros() (or gen_kind / seed as in the _ex calls, graph g from seed + g), then
+ *      GraphIID::push, i.e. EdgesIID::push (the edge labels sorted by edge index as a tuple
+ *      (i, j), then the ErdosRenyi indicator vector) followed by IID<NodeC>::push of the node
+ *      labels (src/graph_codec.rs:31-34, 61-65); its stream is that message flattened.
+ *      Edges are uint32 pairs in the alphabet of section 5 (undirected: i <= j); an edge outside
+ *      it, or with labelled edges a pair given twice, is ANS_E_SYMBOL; a label outside its table
+ *      is ANS_E_SYMBOL.  Decode pops node labels, the indicator vector, then as many edge labels
+ *      as the vector holds edges (src/graph_codec.rs:36-38, 67-71) and returns every graph's
+ *      edges sorted by (i, j) -- EdgesIID::pop's `indices.sort_unstable()` -- with their labels
+ *      beside them, graph after graph; edge_offsets (num_graphs + 1) gives each graph's range;
+ *      ANS_E_LEN when the edges exceed cap (edge_offsets still complete).
+ * ====================================================================== */
+#define ANS_NO_TABLE 0xFFFFFFFFu
+int ans_gpu_graphs_encode(ans_gpu_tableset *ts, uint32_t node_table, uint32_t edge_table,
+                          uint32_t edge_indicator_table, int directed, int loops, uint64_t num_graphs,
+                          const uint32_t *num_nodes, const uint32_t *node_labels, const uint32_t *edges,
+                          const uint32_t *edge_labels, const uint64_t *edge_offsets, int gen_kind, uint64_t seed,
+                          uint8_t *out, uint64_t out_cap, uint64_t *offsets, uint64_t *lens, uint64_t *total);
+int ans_gpu_graphs_decode(ans_gpu_tableset *ts, uint32_t node_table, uint32_t edge_table,
+                          uint32_t edge_indicator_table, int directed, int loops, uint64_t num_graphs,
+                          const uint32_t *num_nodes, const uint8_t *in, uint64_t in_len, const uint64_t *offsets,
+                          const uint64_t *lens, int gen_kind, uint64_t seed, uint32_t *node_labels, uint32_t *edges,
+                          uint32_t *edge_labels, uint64_t cap, uint64_t *edge_offsets);
 
 #ifdef __cplusplus
 }

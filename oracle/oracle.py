@@ -318,3 +318,52 @@ def codec_decode_chunks(codec, data, offsets, lens, n, chunk_len, param=0, table
         raise RuntimeError(f"oracle codec decode failed rc={rc}")
     return out[:n]
 
+
+
+# ---- GraphIID (src/graph_codec.rs:19-94) composed literally from the oracle's codecs
+def _label_push(m, label, xs):
+    """IID<label>::push of xs (src/codec.rs:415-420): ('cat', masses) or ('uniform', size)."""
+    kind, p = label
+    if kind == "cat":
+        return Categorical(p).push_iid(m, xs)
+    for x in reversed(list(xs)):
+        rc = uniform_push(m, p, int(x))
+        if rc:
+            return rc
+    return 0
+
+
+def _label_pop(m, label, n):
+    kind, p = label
+    if kind == "cat":
+        return [int(v) for v in Categorical(p).pop_iid(m, n)]
+    return [uniform_pop(m, p) for _ in range(n)]
+
+
+def graph_iid_push(m, num_nodes, node_labels, edges, edge_labels, bern_masses, node, edge, directed, loops):
+    """GraphIID::push (src/graph_codec.rs:31-34) on the oracle message m: EdgesIID::push (61-65:
+    the labels sorted by the edge index tuple, IID-pushed, then the ErdosRenyi indicator vector),
+    then IID<NodeC>::push of the node labels.  node / edge: None (EmptyCodec), ('cat', masses) or
+    ('uniform', size).  Returns the first nonzero status."""
+    order = sorted(range(len(edges)), key=lambda k: (int(edges[k][0]), int(edges[k][1])))
+    if edge is not None:
+        rc = _label_push(m, edge, [int(edge_labels[k]) for k in order])
+        if rc:
+            return rc
+    rc = Categorical(bern_masses).push_iid(m, dense_set(np.asarray(edges).reshape(-1, 2), num_nodes, directed, loops))
+    if rc:
+        return rc
+    if node is not None:
+        return _label_push(m, node, [int(x) for x in node_labels])
+    return 0
+
+
+def graph_iid_pop(m, num_nodes, bern_masses, node, edge, directed, loops):
+    """GraphIID::pop (src/graph_codec.rs:36-38, 67-71): (node labels, edges sorted by (i, j),
+    their labels)."""
+    nodes = _label_pop(m, node, num_nodes) if node is not None else None
+    alpha = all_edge_indices(num_nodes, directed, loops)
+    dense = Categorical(bern_masses).pop_iid(m, len(alpha))
+    indices = sorted(a for a, b in zip(alpha, dense) if b)
+    labels = _label_pop(m, edge, len(indices)) if edge is not None else None
+    return nodes, indices, labels

@@ -134,7 +134,16 @@ SIGNATURES = {
     "ans_gpu_decode_var_chunks": (ci, [vp, vp, u64, vp, vp, u64, vp, ci, vp, ci]),
     "ans_gpu_dense_sets_encode": (ci, [vp, u64, vp, ci, ci, vp, vp, vp, u64, vp, vp, u64p]),
     "ans_gpu_dense_sets_decode": (ci, [vp, u64, vp, ci, ci, vp, u64, vp, vp, vp, u64, vp]),
+    "ans_gpu_independent_encode_var_chunks": (ci, [vp, vp, vp, ci, u64, vp, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_independent_decode_var_chunks": (ci, [vp, vp, vp, u64, vp, vp, u64, vp, ci, u64, vp, ci]),
+    "ans_dev_independent_encode_var": (ci, [vp, vp, vp, ci, u64, vp, ci, u64, vp, u64, vp, vp, vp]),
+    "ans_dev_independent_decode_var": (ci, [vp, vp, vp, vp, u64, vp, u64, vp, ci, u64, vp, ci, vp, vp]),
+    "ans_gpu_graphs_encode": (ci, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ci, ci, u64, vp, vp, vp, vp,
+                                   vp, ci, u64, vp, u64, vp, vp, u64p]),
+    "ans_gpu_graphs_decode": (ci, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ci, ci, u64, vp, vp, u64, vp,
+                                   vp, ci, u64, vp, vp, vp, u64, vp]),
 }
+ANS_NO_TABLE = 0xFFFFFFFF
 
 _lib = None
 
@@ -942,6 +951,38 @@ class GpuTableSet:
                "ans_gpu_independent_decode_chunks")
         return out[:n]
 
+    def encode_var_chunks(self, table_ids, syms, starts, gen_kind=GEN_ZEROS, seed=0):
+        """Chunk c = positions [starts[c], starts[c+1]), one message each (the exact kernels)."""
+        syms = np.ascontiguousarray(syms)
+        tids = np.ascontiguousarray(np.asarray(table_ids, dtype=np.uint32))
+        st = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
+        nchunks = len(st) - 1
+        longest = int(np.max(np.diff(st))) if nchunks else 0
+        cap = max(nchunks * self.slot_capacity(max(longest, 1)), 1)
+        out = np.empty(cap, np.uint8)
+        offsets = np.zeros(max(nchunks, 1), np.uint64)
+        lens = np.zeros(max(nchunks, 1), np.uint64)
+        total = u64(0)
+        _check(lib().ans_gpu_independent_encode_var_chunks(self.h, _np_ptr(tids), _np_ptr(syms), _WIDTH[syms.dtype],
+                                                           nchunks, _np_ptr(st), gen_kind, seed, _np_ptr(out), cap,
+                                                           _np_ptr(offsets), _np_ptr(lens), ctypes.byref(total)),
+               "ans_gpu_independent_encode_var_chunks")
+        return out[:total.value], offsets[:nchunks], lens[:nchunks]
+
+    def decode_var_chunks(self, table_ids, data, offsets, lens, starts, dtype=np.uint32, gen_kind=GEN_ZEROS, seed=0):
+        data, offsets, lens = _dec_arrays(data, offsets, lens)
+        tids = np.ascontiguousarray(np.asarray(table_ids, dtype=np.uint32))
+        st = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
+        nchunks = len(st) - 1
+        n = int(st[-1]) if nchunks else 0
+        out = np.zeros(max(n, 1), dtype)
+        _check(lib().ans_gpu_independent_decode_var_chunks(self.h, _np_ptr(tids), _np_ptr(data) if data.size else None,
+                                                           data.size, _np_ptr(offsets), _np_ptr(lens), nchunks,
+                                                           _np_ptr(st), gen_kind, seed, _np_ptr(out),
+                                                           _WIDTH[np.dtype(dtype)]),
+               "ans_gpu_independent_decode_var_chunks")
+        return out[:n]
+
     def fast(self):
         """1 / 2: the set runs on the fast kernels (2: with voted exact renorm rows); 0: exact only."""
         f = ci(0)
@@ -1137,6 +1178,166 @@ class GpuDenseSets:
             _check(rc, "ans_gpu_dense_sets_decode")
             return [edges[int(eo[g]):int(eo[g + 1])] for g in range(len(nn))]
         raise AnsError(ANS_E_LEN, "ans_gpu_dense_sets_decode")
+
+
+class EmptyCodec(Codec):
+    """ConstantCodec<()> (src/codec.rs, graph_codec.rs:16 EmptyCodec): codes nothing."""
+
+    def push(self, m, x):
+        pass
+
+    def pop(self, m):
+        return None
+
+    def bits(self, x):
+        return 0.0
+
+
+class Graph(collections.namedtuple("Graph", "node_labels edges")):
+    """Graph<N, E, Ty> as GraphIID codes it (src/graph.rs:89-168): node_labels (one per node;
+    None entries for EmptyCodec nodes) and edges, a list of ((i, j), label) (label None for
+    unlabelled edges; undirected pairs have i <= j)."""
+
+    def __len__(self):
+        return len(self.node_labels)
+
+
+class EdgesIID(Codec):  # src/graph_codec.rs:51-94
+    def __init__(self, indices, label=None):
+        self.indices = indices
+        self.label = label if label is not None else EmptyCodec()
+
+    @staticmethod
+    def split(x):  # src/graph_codec.rs:82-85: sorted by the edge index (a tuple)
+        s = sorted(((tuple(map(int, i)), l) for i, l in x), key=lambda e: e[0])
+        return [e[0] for e in s], [e[1] for e in s]
+
+    def push(self, m, x):  # src/graph_codec.rs:61-65
+        indices, labels = self.split(x)
+        IID(self.label, len(indices)).push(m, labels)
+        self.indices.push(m, indices)
+
+    def pop(self, m):  # src/graph_codec.rs:67-71
+        indices = sorted(self.indices.pop(m))
+        labels = IID(self.label, len(indices)).pop(m)
+        return list(zip(indices, labels))
+
+    def bits(self, x):
+        indices, labels = self.split(x)
+        a, b = self.indices.bits(indices), IID(self.label, len(indices)).bits(labels)
+        return None if a is None or b is None else a + b
+
+
+class GraphIID(Codec):  # src/graph_codec.rs:19-49
+    """GraphIID::new(num_nodes, edge_indices, node, edge): the node labels IID, the edges through
+    EdgesIID; None for node / edge is EmptyCodec."""
+
+    def __init__(self, num_nodes, edge_indices, node=None, edge=None):
+        self.nodes = IID(node if node is not None else EmptyCodec(), num_nodes)
+        self.edges = EdgesIID(edge_indices, edge)
+
+    def push(self, m, x):  # src/graph_codec.rs:31-34
+        self.edges.push(m, x.edges)
+        self.nodes.push(m, list(x.node_labels))
+
+    def pop(self, m):  # src/graph_codec.rs:36-38
+        nodes = self.nodes.pop(m)
+        return Graph(nodes, self.edges.pop(m))
+
+    def bits(self, x):
+        a, b = self.nodes.bits(list(x.node_labels)), self.edges.bits(x.edges)
+        return None if a is None or b is None else a + b
+
+
+def _label_categorical(c):
+    """A label codec as the Categorical the GPU table set holds: Uniform(size) becomes the all-ones
+    Categorical of that size (pmf 1, cdf x, norm size: Uniform's arithmetic)."""
+    if c is None or isinstance(c, EmptyCodec):
+        return None
+    if isinstance(c, Categorical):
+        return c
+    if isinstance(c, Uniform):
+        return Categorical(np.ones(c.size, np.uint64))
+    raise TypeError(f"no GPU table for {type(c).__name__}")
+
+
+class GpuGraphs:
+    """Independent<GraphIID<NodeC, EdgeC, ErdosRenyi>> over a dataset on the GPU (section 5b of
+    the C ABI): every graph's message is GraphIID::push of that graph on Message::zeros(), with one
+    Bernoulli for the edge indicators and Categorical (or Uniform) node / edge labels, as the
+    reference's --er / --uniform-er models build them (src/benchmark.rs:308-372)."""
+
+    def __init__(self, gpu, edge, node=None, edge_label=None, directed=False, loops=False):
+        self.gpu = gpu
+        self.edge = edge
+        self.node_cat, self.edge_cat = _label_categorical(node), _label_categorical(edge_label)
+        tables = [edge.categorical] + [c for c in (self.node_cat, self.edge_cat) if c is not None]
+        self.tableset = GpuTableSet(gpu, tables)
+        self.t_node = 1 if self.node_cat is not None else ANS_NO_TABLE
+        self.t_edge = (2 if self.node_cat is not None else 1) if self.edge_cat is not None else ANS_NO_TABLE
+        self.directed, self.loops = int(bool(directed)), int(bool(loops))
+
+    def fast(self):
+        return self.tableset.fast()
+
+    def _sizes(self, num_nodes):
+        return [len(AllEdgeIndices(int(n), self.directed, self.loops)) for n in num_nodes]
+
+    def encode(self, graphs, gen_kind=GEN_ZEROS, seed=0):
+        """graphs: per graph (num_nodes, node_labels or None, edges (m, 2), edge_labels or None).
+        Returns (bytes, offsets, lens), one stream per graph."""
+        nn = np.ascontiguousarray(np.asarray([int(g[0]) for g in graphs], dtype=np.uint32))
+        nl = [np.asarray(g[1] if g[1] is not None else np.zeros(0), dtype=np.uint32).reshape(-1) for g in graphs]
+        parts = [np.asarray(g[2], dtype=np.uint32).reshape(-1, 2) for g in graphs]
+        el = [np.asarray(g[3] if g[3] is not None else np.zeros(0), dtype=np.uint32).reshape(-1) for g in graphs]
+        eo = np.zeros(len(parts) + 1, np.uint64)
+        eo[1:] = np.cumsum([len(p) for p in parts])
+        edges = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros((0, 2), np.uint32))
+        node_labels = np.ascontiguousarray(np.concatenate(nl) if nl else np.zeros(0, np.uint32))
+        edge_labels = np.ascontiguousarray(np.concatenate(el) if el else np.zeros(0, np.uint32))
+        sizes = self._sizes(nn)
+        longest = max([int(n) + s + len(p) for n, s, p in zip(nn, sizes, parts)] + [1])
+        cap = max(len(nn) * self.tableset.slot_capacity(longest), 1)
+        out = np.empty(cap, np.uint8)
+        offsets = np.zeros(max(len(nn), 1), np.uint64)
+        lens = np.zeros(max(len(nn), 1), np.uint64)
+        total = u64(0)
+        _check(lib().ans_gpu_graphs_encode(self.tableset.h, self.t_node, self.t_edge, 0, self.directed, self.loops,
+                                           len(nn), _np_ptr(nn), _np_ptr(node_labels) if node_labels.size else None,
+                                           _np_ptr(edges), _np_ptr(edge_labels) if edge_labels.size else None,
+                                           _np_ptr(eo), gen_kind, seed, _np_ptr(out), cap, _np_ptr(offsets),
+                                           _np_ptr(lens), ctypes.byref(total)), "ans_gpu_graphs_encode")
+        return out[:total.value], offsets[:len(nn)], lens[:len(nn)]
+
+    def decode(self, num_nodes, data, offsets, lens, cap=None, gen_kind=GEN_ZEROS, seed=0):
+        """Per graph (node_labels or None, edges sorted by (i, j), edge_labels or None)."""
+        nn = np.ascontiguousarray(np.asarray(num_nodes, dtype=np.uint32))
+        data, offsets, lens = _dec_arrays(data, offsets, lens)
+        slots = sum(self._sizes(nn))
+        if cap is None:
+            cap = int(2 * self.edge.prob() * slots) + 1024
+        cap = min(cap, slots)
+        node_labels = np.zeros(max(int(nn.sum()), 1), np.uint32)
+        eo = np.zeros(len(nn) + 1, np.uint64)
+        for _ in range(2):
+            edges = np.zeros((max(cap, 1), 2), np.uint32)
+            edge_labels = np.zeros(max(cap, 1), np.uint32)
+            rc = lib().ans_gpu_graphs_decode(self.tableset.h, self.t_node, self.t_edge, 0, self.directed, self.loops,
+                                             len(nn), _np_ptr(nn), _np_ptr(data) if data.size else None, data.size,
+                                             _np_ptr(offsets), _np_ptr(lens), gen_kind, seed, _np_ptr(node_labels),
+                                             _np_ptr(edges), _np_ptr(edge_labels), cap, _np_ptr(eo))
+            if rc == ANS_E_LEN and int(eo[-1]) > cap:
+                cap = int(eo[-1])
+                continue
+            _check(rc, "ans_gpu_graphs_decode")
+            no = np.concatenate([[0], np.cumsum(nn.astype(np.uint64))]).astype(np.int64)
+            out = []
+            for g in range(len(nn)):
+                a, b = int(eo[g]), int(eo[g + 1])
+                out.append((node_labels[no[g]:no[g + 1]].copy() if self.node_cat is not None else None,
+                            edges[a:b].copy(), edge_labels[a:b].copy() if self.edge_cat is not None else None))
+            return out
+        raise AnsError(ANS_E_LEN, "ans_gpu_graphs_decode")
 
 
 # ============================================================== synthetic tables (SURVEY.md §8d)

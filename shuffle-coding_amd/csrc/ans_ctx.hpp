@@ -6,6 +6,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <new>
+#include <stdexcept>
 
 #include "ans_fast.hpp"
 #include "ans_table.hpp"
@@ -75,6 +77,17 @@ struct ans_gpu_table {
         }                                                                                              \
     } while (0)
 
+// No C++ exception crosses the C ABI: every extern "C" entry of the HIP units
+// is a function-try-block ending in ANS_CATCH.  A host allocation that fails (std::bad_alloc, or
+// std::length_error from a std::vector sized by caller input) is ANS_E_ALLOC; anything else that
+// escapes is ANS_E_ARG.  (ans_capi.cpp's host entries do the same through guarded().)
+#define ANS_CATCH                                         \
+    catch (const std::bad_alloc&) { return ANS_E_ALLOC; } \
+    catch (const std::length_error&) { return ANS_E_ALLOC; } \
+    catch (...) { return ANS_E_ARG; }
+#define ANS_CATCH_VOID \
+    catch (...) {}
+
 // Variable-chunk encode of device-resident symbols into a host container (ans_kernels.hip):
 // the body of ans_gpu_encode_var_chunks; starts is a host array of nchunks + 1 entries.
 int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
@@ -86,6 +99,7 @@ int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_by
 int ans_tableset_build(ans_gpu* g, const Categorical* const* cats, uint32_t ntables, struct ans_gpu_tableset** out);
 void ans_tableset_destroy(struct ans_gpu_tableset* ts);
 uint64_t ans_tableset_slot_bytes(const struct ans_gpu_tableset* ts, uint64_t chunk_len);
+ans_gpu* ans_tableset_gpu(const struct ans_gpu_tableset* ts);
 int ans_tableset_dev_encode(struct ans_gpu_tableset* ts, const void* d_syms, int w, const uint64_t* d_starts, uint64_t n,
                             uint64_t chunk_len, uint64_t nchunks, uint8_t* d_slots, uint64_t slot_cap,
                             uint32_t* d_lens, uint32_t* d_status, int gen_kind, uint64_t seed, void* stream);
@@ -99,6 +113,28 @@ int ans_tableset_host_encode(struct ans_gpu_tableset* ts, const void* syms, int 
 int ans_tableset_host_decode(struct ans_gpu_tableset* ts, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                              const uint64_t* lens, uint64_t n, uint64_t chunk_len, const uint64_t* starts,
                              uint64_t nchunks, int gen_kind, uint64_t seed, void* out, int w);
+
+// GraphIID<NodeC, EdgeC, ErdosRenyi> per graph over a table set (ans_codecs.hip
+// k_graph_encode64 / k_graph_decode64; composed by ans_graph.hip).  Graph g's node labels are
+// [node_off[g], node_off[g+1]) of the node-label array, its edge-indicator slots (AllEdgeIndices
+// order) [slot_off[g], slot_off[g+1]) of the dense vector, and (encode) its edge labels sorted by
+// edge index [edge_off[g], edge_off[g+1]).  kNoTable: no node / edge labels (EmptyCodec).
+constexpr uint32_t kNoTable = 0xFFFFFFFFu;
+struct GraphLayout {
+    const uint64_t* node_off;
+    const uint64_t* slot_off;
+    const uint64_t* edge_off;
+    uint32_t t_node, t_edge, t_bern;
+};
+int ans_tableset_graph_encode(struct ans_gpu_tableset* ts, const GraphLayout& gl, uint64_t num_graphs,
+                              const uint32_t* d_node_labels, const uint8_t* d_dense, const uint32_t* d_edge_labels,
+                              int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
+                              uint32_t* d_status, hipStream_t s);
+// edge labels land in pop order at d_edge_scratch[slot_off[g] ..]; d_edge_count[g] = graph g's edges
+int ans_tableset_graph_decode(struct ans_gpu_tableset* ts, const GraphLayout& gl, uint64_t num_graphs,
+                              const uint8_t* d_in, const uint64_t* d_offsets, const uint32_t* d_lens, int gen_kind,
+                              uint64_t seed, uint32_t* d_node_labels, uint8_t* d_dense, uint32_t* d_edge_scratch,
+                              uint64_t* d_edge_count, uint32_t* d_status, hipStream_t s);
 
 // Variable-length chunks with the longest chunk's length known to the caller (lmax > 0): the
 // staged fast kernels where the table has them (ans_kernels.hip launch_staged_*), else generic.

@@ -386,7 +386,9 @@ struct PageOut {
 // kVar (LDS rows only): chunk c holds vlen[c] <= chunk_len symbols at the start of its stride
 // (staged ragged / variable-length chunks, ans_kernels.hip launch_staged_encode); the pushes
 // past vlen[c], all in its first-coded group, are skipped.
-// kNR: the norm range (kNormStd / kNormSmall / kNormBig above; LDS rows only for the latter two).
+// kNR: the norm range (kNormStd / kNormSmall / kNormBig above).  kNormSmall also runs with global
+// rows (more than 256 symbols below 2^16: a count-built label table, src/benchmark.rs:576-578);
+// kNormBig's large alphabets take k_encode_w (norm >= kWideNormMin).
 // kM24 (LDS rows, kNormStd): every mass is below 2^24, so a row's mass word carries 8 k0 in its
 // top byte and its renorm word is T - 1: head >= T is then head > T - 1 on the head's own
 // register pair (r05; the (head | 0xFF) > T + 8 k0 form needed a v_or and a v_mov of the high
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
                                                                          uint32_t* __restrict__ status, ChunkInit ini,
                                                                          const uint32_t* __restrict__ vlen = nullptr) {
     static_assert(!(kVar && kGlobalRows), "staged chunks take the LDS-row kernel");
-    static_assert(kNR == kNormStd || !kGlobalRows, "other norm ranges: LDS rows only");
+    static_assert(kNR != kNormBig || !kGlobalRows, "2^31 < norm: the large-alphabet rows take k_encode_w");
     static_assert(!kM24 || (!kGlobalRows && kNR == kNormStd), "kM24: the LDS rows of the standard range");
     extern __shared__ __align__(16) unsigned char lds[];
     // a symbol's row is two random LDS reads: rcp by ds_read_b64 (32-lane groups over 32 bank
@@ -1469,12 +1471,14 @@ struct DecChainG {
             fetch_page(low - 2, S1);
         }
     }
-    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
+    template <int kNR = kNormStd>
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm,
+                                               double neg_norm = 0.0) {
         form_window();
         P -= static_cast<int32_t>(renorm_up(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's bucket reads
         __builtin_amdgcn_sched_barrier(0);
-        div_norm(head, norm, rcp_norm, qq, cf);
+        div_norm<kNR>(head, norm, rcp_norm, qq, cf, neg_norm);
     }
     __device__ __forceinline__ void lookup(const DecBucketG* __restrict__ bkt, uint32_t shift) {
         const uint4* e = reinterpret_cast<const uint4*>(bkt + (cf >> shift));
@@ -1498,7 +1502,8 @@ struct DecChainG {
     __device__ __forceinline__ void update() { head = qq * (nxt - cum) + (cf - cum); }
 };
 
-template <typename Sym>
+// kNR: the norm range (div_norm: kNormSmall's long division, kNormBig's 64-bit remainder)
+template <typename Sym, int kNR = kNormStd>
 __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8_t* __restrict__ slots,
                                                         uint64_t slot_cap, const uint64_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ lens,
@@ -1544,7 +1549,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decode_g(FastTable t, const uint8
             uint4 outv = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < U; ++j) {
-                ch.renorm_div(L, hL8, norm, rcp_norm);
+                ch.template renorm_div<kNR>(L, hL8, norm, rcp_norm, -static_cast<double>(norm));
                 ch.lookup(t.dbkt_g, shift);
                 if (__builtin_expect(__any(ch.far), 0)) ch.lookup_far(t.cum);
                 ch.update();

@@ -267,16 +267,17 @@ static double rcp_up(uint32_t d) {
     return r;
 }
 
-// Derives the fast-path tables (ans_table.hpp FastTable) when the table qualifies:
-// nsym <= 65536 with 2^16 <= norm <= 2^31 (f64 quotient estimate), or nsym <= 256
-// at any other norm (the LDS kernels' kNormSmall / kNormBig division).  Up to 256
-// symbols the rows and decode buckets are staged in LDS; above, the encoder reads its rows
-// from global memory and decoding uses the generic kernel.
+// Derives the fast-path tables (ans_table.hpp FastTable) when the table qualifies: nsym <= 65536
+// and norm < 2^32, in one of the three norm ranges (2^16 <= norm <= 2^31: one f64 quotient
+// estimate; below 2^16 or above 2^31: the kNormSmall / kNormBig division of
+// DESIGN.md §4b, in the LDS kernels and the large-alphabet ones alike).  Up to 256 symbols the
+// rows and decode buckets are staged in LDS; above, the encoder reads its rows from global memory
+// (k_encode with global rows, or k_encode_w from 2^22 on) and decodes take k_decode_w / k_decode_g.
 int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const DevTable& t = gt->t;
     FastTable ft{};
     const uint32_t nr = t.fast ? fast::kNormStd : (t.norm < (1u << 16) ? fast::kNormSmall : fast::kNormBig);
-    if (t.nsym > (nr == fast::kNormStd ? 65536u : 256u)) {
+    if (t.nsym > 65536u) {
         gt->ft = ft;
         return ANS_OK;
     }
@@ -1258,15 +1259,15 @@ int ans_encode_var_from_device(ans_gpu_table* gt, const void* d_syms, int sym_by
 // ====================================================================== C ABI (GPU part)
 extern "C" {
 
-int ans_gpu_device_count(int* count) {
+int ans_gpu_device_count(int* count) try {
     if (!count) return ANS_E_ARG;
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
     *count = c;
     return ANS_OK;
-}
+} ANS_CATCH
 
-int ans_gpu_create(int device, ans_gpu** out) {
+int ans_gpu_create(int device, ans_gpu** out) try {
     if (!out) return ANS_E_ARG;
     *out = nullptr;
     int count = 0;
@@ -1282,9 +1283,9 @@ int ans_gpu_create(int device, ans_gpu** out) {
     }
     *out = g;
     return ANS_OK;
-}
+} ANS_CATCH
 
-int ans_host_alloc(size_t bytes, void** out) {
+int ans_host_alloc(size_t bytes, void** out) try {
     if (!out) return ANS_E_ARG;
     *out = nullptr;
     if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
@@ -1292,34 +1293,34 @@ int ans_host_alloc(size_t bytes, void** out) {
         return ANS_E_ALLOC;
     }
     return ANS_OK;
-}
+} ANS_CATCH
 
-void ans_host_free(void* p) {
+void ans_host_free(void* p) try {
     if (p) (void)hipHostFree(p);
-}
+} ANS_CATCH_VOID
 
-int ans_gpu_set_batch_bytes(ans_gpu* g, uint64_t batch_bytes) {
+int ans_gpu_set_batch_bytes(ans_gpu* g, uint64_t batch_bytes) try {
     if (!g) return ANS_E_ARG;
     g->batch_bytes = batch_bytes;
     return ANS_OK;
-}
+} ANS_CATCH
 
-int ans_gpu_pipe_depth(const ans_gpu* g, int* depth) {
+int ans_gpu_pipe_depth(const ans_gpu* g, int* depth) try {
     if (!g || !depth) return ANS_E_ARG;
     *depth = g->pipe ? g->pipe->depth : 0;
     return ANS_OK;
-}
+} ANS_CATCH
 
-void ans_gpu_free(ans_gpu* g) {
+void ans_gpu_free(ans_gpu* g) try {
     if (!g) return;
     (void)hipSetDevice(g->device);
     pipe_free(g);
     if (g->d_scratch) (void)hipFree(g->d_scratch);
     (void)hipStreamDestroy(g->stream);
     delete g;
-}
+} ANS_CATCH_VOID
 
-int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) {
+int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) try {
     if (!g || !tab || !out) return ANS_E_ARG;
     *out = nullptr;
     const Categorical& cat = tab->cat;
@@ -1383,18 +1384,18 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
     }
     *out = gt;
     return ANS_OK;
-}
+} ANS_CATCH
 
-void ans_gpu_table_free(ans_gpu_table* gt) {
+void ans_gpu_table_free(ans_gpu_table* gt) try {
     if (!gt) return;
     (void)hipSetDevice(gt->g->device);
     if (gt->ts64) ans_tableset_destroy(gt->ts64);
     if (gt->d_mem) (void)hipFree(gt->d_mem);
     if (gt->d_fast) (void)hipFree(gt->d_fast);
     delete gt;
-}
+} ANS_CATCH_VOID
 
-int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
+int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) try {
     if (!gt || !paths) return ANS_E_ARG;
     const FastTable& ft = gt->ft;
     uint32_t p = 0;
@@ -1409,9 +1410,9 @@ int ans_gpu_table_paths(const ans_gpu_table* gt, uint32_t* paths) {
     if (ft.usable && ft.dec_usable && !ft.dec_far && ft.dec_u) p |= ANS_PATH_DEC_U;
     *paths = p;
     return ANS_OK;
-}
+} ANS_CATCH
 
-int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t* slot_cap) {
+int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t* slot_cap) try {
     if (!gt || !slot_cap) return ANS_E_ARG;
     if (gt->ts64) {
         *slot_cap = ans_tableset_slot_bytes(gt->ts64, chunk_len);
@@ -1426,11 +1427,11 @@ int ans_gpu_slot_capacity(const ans_gpu_table* gt, uint64_t chunk_len, uint64_t*
     const uint64_t cap = static_cast<uint64_t>(std::ceil(bytes)) + 8 + 64;
     *slot_cap = (cap + 127) & ~uint64_t(127);
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_dev_encode_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                              int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
-                             uint32_t* d_status, void* stream) {
+                             uint32_t* d_status, void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0 || (slot_cap & 15) || !valid_kind(gen_kind))
         return ANS_E_ARG;
@@ -1446,17 +1447,17 @@ int ans_dev_encode_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_byte
     case 2: return launch_encode<uint16_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s, ini);
     default: return launch_encode<uint32_t>(gt, d_syms, n, chunk_len, d_slots, slot_cap, d_lens, d_status, s, ini);
     }
-}
+} ANS_CATCH
 
 int ans_dev_encode_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
-                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) try {
     return ans_dev_encode_chunks_ex(gt, d_syms, sym_bytes, n, chunk_len, ANS_GEN_ZEROS, 0, d_slots, slot_cap, d_lens,
                                     d_status, stream);
-}
+} ANS_CATCH
 
 int ans_dev_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                              const uint32_t* d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
-                             void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+                             void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || chunk_len == 0 || !valid_kind(gen_kind)) return ANS_E_ARG;
     if (n && (!d_in || !d_lens || !d_syms)) return ANS_E_ARG;
@@ -1473,18 +1474,18 @@ int ans_dev_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint6
     case 2: return launch_decode<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s, ini);
     default: return launch_decode<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, d_syms, d_status, s, ini);
     }
-}
+} ANS_CATCH
 
 int ans_dev_decode_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                           const uint32_t* d_lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* d_syms,
-                          int sym_bytes, uint32_t* d_status, void* stream) {
+                          int sym_bytes, uint32_t* d_status, void* stream) try {
     if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
     return ans_dev_decode_chunks_ex(gt, d_in, d_offsets, slot_cap, d_lens, n, chunk_len, gen_kind, 0, d_syms, sym_bytes,
                                     d_status, stream);
-}
+} ANS_CATCH
 
 int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n, void* d_syms, int sym_bytes,
-                    void* stream) {
+                    void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || (n && !d_syms)) return ANS_E_ARG;
     if (gt->ts64) return ANS_E_NORM_RANGE;  // the synthetic generator reads u32 tables
@@ -1496,10 +1497,10 @@ int ans_dev_gen_iid(ans_gpu_table* gt, uint64_t seed, uint64_t start, uint64_t n
     case 2: return launch_gen<uint16_t>(gt, seed, start, n, d_syms, s);
     default: return launch_gen<uint32_t>(gt, seed, start, n, d_syms, s);
     }
-}
+} ANS_CATCH
 
 int ans_dev_check_renorm(ans_gpu* g, const uint64_t* d_heads, const uint32_t* d_windows, uint64_t L, uint64_t n,
-                         uint64_t* d_out_heads, uint32_t* d_out_k, void* stream) {
+                         uint64_t* d_out_heads, uint32_t* d_out_k, void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g || (n && (!d_heads || !d_windows || !d_out_heads || !d_out_k))) return ANS_E_ARG;
     if (n == 0) return ANS_OK;
@@ -1508,10 +1509,10 @@ int ans_dev_check_renorm(ans_gpu* g, const uint64_t* d_heads, const uint32_t* d_
     k_check_renorm<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(d_heads, d_windows, L, n, d_out_heads, d_out_k);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* d_syms, int sym_bytes,
-                       void* stream) {
+                       void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !d_syms)) return ANS_E_ARG;
     if (gt->ts64) return ANS_E_NORM_RANGE;  // the sampler reads u32 tables
@@ -1524,9 +1525,9 @@ int ans_dev_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
     case 2: return launch_sample<uint16_t>(gt, seed, n, chunk_len, d_syms, s);
     default: return launch_sample<uint32_t>(gt, seed, n, chunk_len, d_syms, s);
     }
-}
+} ANS_CATCH
 
-int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* out, int sym_bytes) {
+int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t chunk_len, void* out, int sym_bytes) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || (n && !out)) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(gt->g->device));
@@ -1537,7 +1538,7 @@ int ans_gpu_sample_iid(ans_gpu_table* gt, uint64_t seed, uint64_t n, uint64_t ch
     if (n) HIP_TRY(hipMemcpyAsync(out, d.p, n * sym_bytes, hipMemcpyDeviceToHost, gt->g->stream));
     HIP_TRY(hipStreamSynchronize(gt->g->stream));
     return ANS_OK;
-}
+} ANS_CATCH
 
 // The longest variable chunk and the total of device-resident starts (one workgroup: a strided
 // max per lane, a wave shfl_xor reduction, the 16 wave maxima through LDS) -> out[0], out[1].
@@ -1586,7 +1587,7 @@ static int device_lmax(const uint64_t* d_starts, uint64_t nchunks, int sym_bytes
 // (launch_staged_encode); the device API finds it with device_lmax
 int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                           const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap,
-                          uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax) {
+                          uint32_t* d_lens, uint32_t* d_status, void* stream, uint64_t lmax) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || (slot_cap & 15) || !valid_kind(gen_kind)) return ANS_E_ARG;
     if (nchunks && (!d_syms || !d_starts || !d_slots || !d_lens)) return ANS_E_ARG;
@@ -1601,11 +1602,11 @@ int dev_encode_var(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_
     case 2: return launch_encode_var<uint16_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini, lmax);
     default: return launch_encode_var<uint32_t>(gt, d_syms, nchunks, d_starts, d_slots, slot_cap, d_lens, d_status, s, ini, lmax);
     }
-}
+} ANS_CATCH
 
 int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                                  const uint64_t* d_starts, int gen_kind, uint64_t seed, uint8_t* d_slots,
-                                 uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) {
+                                 uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, void* stream) try {
     (void)hipGetLastError();
     if (!gt || !valid_width(sym_bytes)) return ANS_E_ARG;
     if (nchunks && !d_starts) return ANS_E_ARG;
@@ -1617,18 +1618,18 @@ int ans_dev_encode_var_chunks_ex(ans_gpu_table* gt, const void* d_syms, int sym_
     }
     return dev_encode_var(gt, d_syms, sym_bytes, nchunks, d_starts, gen_kind, seed, d_slots, slot_cap, d_lens, d_status,
                           stream, lmax);
-}
+} ANS_CATCH
 
 int ans_dev_encode_var_chunks(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t nchunks,
                               const uint64_t* d_starts, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
-                              uint32_t* d_status, void* stream) {
+                              uint32_t* d_status, void* stream) try {
     return ans_dev_encode_var_chunks_ex(gt, d_syms, sym_bytes, nchunks, d_starts, ANS_GEN_ZEROS, 0, d_slots, slot_cap,
                                         d_lens, d_status, stream);
-}
+} ANS_CATCH
 
 int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                           const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
-                          uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax) {
+                          uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream, uint64_t lmax) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !d_status || !valid_width(sym_bytes) || !valid_kind(gen_kind)) return ANS_E_ARG;
     if (nchunks && (!d_in || !d_lens || !d_starts || !d_syms)) return ANS_E_ARG;
@@ -1644,11 +1645,11 @@ int dev_decode_var(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_off
     case 2: return launch_decode_var<uint16_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini, lmax);
     default: return launch_decode_var<uint32_t>(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, d_syms, d_status, s, ini, lmax);
     }
-}
+} ANS_CATCH
 
 int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                                  const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
-                                 uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+                                 uint64_t seed, void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) try {
     (void)hipGetLastError();
     if (!gt || !valid_width(sym_bytes)) return ANS_E_ARG;
     if (nchunks && !d_starts) return ANS_E_ARG;
@@ -1660,19 +1661,19 @@ int ans_dev_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* d_in, const u
     }
     return dev_decode_var(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, seed, d_syms, sym_bytes,
                           d_status, stream, lmax);
-}
+} ANS_CATCH
 
 int ans_dev_decode_var_chunks(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offsets, uint64_t slot_cap,
                               const uint32_t* d_lens, uint64_t nchunks, const uint64_t* d_starts, int gen_kind,
-                              void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) {
+                              void* d_syms, int sym_bytes, uint32_t* d_status, void* stream) try {
     if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
     return ans_dev_decode_var_chunks_ex(gt, d_in, d_offsets, slot_cap, d_lens, nchunks, d_starts, gen_kind, 0, d_syms,
                                         sym_bytes, d_status, stream);
-}
+} ANS_CATCH
 
 int ans_gpu_encode_var_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t nchunks,
                                  const uint64_t* starts, int gen_kind, uint64_t seed, uint8_t* out, uint64_t out_cap,
-                                 uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+                                 uint64_t* offsets, uint64_t* lens, uint64_t* total) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || !total || (nchunks && !starts) || !valid_kind(gen_kind)) return ANS_E_ARG;
     *total = 0;
@@ -1687,18 +1688,18 @@ int ans_gpu_encode_var_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_by
     if (n) HIP_TRY(hipMemcpyAsync(d_syms.p, syms, n * sym_bytes, hipMemcpyHostToDevice, gt->g->stream));
     return ans_encode_var_from_device(gt, d_syms.p, sym_bytes, nchunks, starts, out, out_cap, offsets, lens, total,
                                       gen_kind, seed);
-}
+} ANS_CATCH
 
 int ans_gpu_encode_var_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t nchunks,
                               const uint64_t* starts, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
-                              uint64_t* lens, uint64_t* total) {
+                              uint64_t* lens, uint64_t* total) try {
     return ans_gpu_encode_var_chunks_ex(gt, syms, sym_bytes, nchunks, starts, ANS_GEN_ZEROS, 0, out, out_cap, offsets,
                                         lens, total);
-}
+} ANS_CATCH
 
 int ans_gpu_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                                  const uint64_t* lens, uint64_t nchunks, const uint64_t* starts, int gen_kind,
-                                 uint64_t seed, void* out, int sym_bytes) {
+                                 uint64_t seed, void* out, int sym_bytes) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || (nchunks && (!starts || !offsets || !lens)) || !valid_kind(gen_kind))
         return ANS_E_ARG;
@@ -1737,17 +1738,17 @@ int ans_gpu_decode_var_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t 
     if (st) return st;
     if (n) HIP_TRY(hipMemcpy(out, d_out.p, n * sym_bytes, hipMemcpyDeviceToHost));
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_gpu_decode_var_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                               const uint64_t* lens, uint64_t nchunks, const uint64_t* starts, int gen_kind, void* out,
-                              int sym_bytes) {
+                              int sym_bytes) try {
     if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
     return ans_gpu_decode_var_chunks_ex(gt, in, in_len, offsets, lens, nchunks, starts, gen_kind, 0, out, sym_bytes);
-}
+} ANS_CATCH
 
 int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const uint32_t* d_lens,
-                    const uint64_t* d_offsets, uint64_t nchunks, uint8_t* d_out, void* stream) {
+                    const uint64_t* d_offsets, uint64_t nchunks, uint8_t* d_out, void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g) return ANS_E_ARG;
     if (nchunks == 0) return ANS_OK;
@@ -1756,10 +1757,10 @@ int ans_dev_compact(ans_gpu* g, const uint8_t* d_slots, uint64_t slot_cap, const
     k_compact<<<grid_for(nchunks * 64), kBlock, 0, s>>>(d_slots, slot_cap, d_lens, d_offsets, nchunks, d_out);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_dev_expand(ans_gpu* g, const uint8_t* d_in, const uint64_t* d_offsets, const uint32_t* d_lens,
-                   uint64_t nchunks, uint8_t* d_slots, uint64_t slot_cap, void* stream) {
+                   uint64_t nchunks, uint8_t* d_slots, uint64_t slot_cap, void* stream) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!g) return ANS_E_ARG;
     if (nchunks == 0) return ANS_OK;
@@ -1769,13 +1770,13 @@ int ans_dev_expand(ans_gpu* g, const uint8_t* d_in, const uint64_t* d_offsets, c
     k_expand<<<grid_for(nchunks * 64), kBlock, 0, s>>>(d_in, d_offsets, d_lens, nchunks, d_slots, slot_cap);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
-}
+} ANS_CATCH
 
 uint64_t ans_dense_offsets_entries(uint64_t nchunks) { return nchunks + 1 + (nchunks + kScanTile - 1) / kScanTile; }
 
 int ans_dev_encode_dense_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                             int gen_kind, uint64_t seed, uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens,
-                            uint64_t* d_offsets, uint8_t* d_out, uint64_t out_cap, uint32_t* d_status, void* stream) {
+                            uint64_t* d_offsets, uint8_t* d_out, uint64_t out_cap, uint32_t* d_status, void* stream) try {
     if (n && (!d_offsets || !d_out)) return ANS_E_ARG;
     int rc = ans_dev_encode_chunks_ex(gt, d_syms, sym_bytes, n, chunk_len, gen_kind, seed, d_slots, slot_cap, d_lens,
                                       d_status, stream);
@@ -1794,16 +1795,16 @@ int ans_dev_encode_dense_ex(ans_gpu_table* gt, const void* d_syms, int sym_bytes
                                                               d_out, out_cap, d_status);
     HIP_TRY(hipGetLastError());
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_dev_encode_dense(ans_gpu_table* gt, const void* d_syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint64_t* d_offsets, uint8_t* d_out,
-                         uint64_t out_cap, uint32_t* d_status, void* stream) {
+                         uint64_t out_cap, uint32_t* d_status, void* stream) try {
     return ans_dev_encode_dense_ex(gt, d_syms, sym_bytes, n, chunk_len, ANS_GEN_ZEROS, 0, d_slots, slot_cap, d_lens,
                                    d_offsets, d_out, out_cap, d_status, stream);
-}
+} ANS_CATCH
 
-int ans_dev_status(ans_gpu* g, const uint32_t* d_status, void* stream, int* status) {
+int ans_dev_status(ans_gpu* g, const uint32_t* d_status, void* stream, int* status) try {
     if (!g || !d_status || !status) return ANS_E_ARG;
     HIP_TRY(hipSetDevice(g->device));
     const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g->stream;
@@ -1812,11 +1813,11 @@ int ans_dev_status(ans_gpu* g, const uint32_t* d_status, void* stream, int* stat
     HIP_TRY(hipStreamSynchronize(s));
     *status = lowest_status(bits);
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_gpu_encode_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
                              int gen_kind, uint64_t seed, uint8_t* out, uint64_t out_cap, uint64_t* offsets,
-                             uint64_t* lens, uint64_t* total) {
+                             uint64_t* lens, uint64_t* total) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0 || !total || !valid_kind(gen_kind)) return ANS_E_ARG;
     const fast::ChunkInit ini{gen_kind, seed};
@@ -1847,17 +1848,17 @@ int ans_gpu_encode_chunks_ex(ans_gpu_table* gt, const void* syms, int sym_bytes,
     case 2: return pipe_encode<uint16_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total, ini);
     default: return pipe_encode<uint32_t>(gt, syms, n, chunk_len, out, out_cap, offsets, lens, total, ini);
     }
-}
+} ANS_CATCH
 
 int ans_gpu_encode_chunks(ans_gpu_table* gt, const void* syms, int sym_bytes, uint64_t n, uint64_t chunk_len,
-                          uint8_t* out, uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) {
+                          uint8_t* out, uint64_t out_cap, uint64_t* offsets, uint64_t* lens, uint64_t* total) try {
     return ans_gpu_encode_chunks_ex(gt, syms, sym_bytes, n, chunk_len, ANS_GEN_ZEROS, 0, out, out_cap, offsets, lens,
                                     total);
-}
+} ANS_CATCH
 
 int ans_gpu_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                              const uint64_t* lens, uint64_t n, uint64_t chunk_len, int gen_kind, uint64_t seed,
-                             void* out, int sym_bytes) {
+                             void* out, int sym_bytes) try {
     (void)hipGetLastError();  // drop a stale error another caller left on this thread
     if (!gt || !valid_width(sym_bytes) || chunk_len == 0) return ANS_E_ARG;
     const uint64_t nchunks = (n + chunk_len - 1) / chunk_len;
@@ -1925,13 +1926,13 @@ int ans_gpu_decode_chunks_ex(ans_gpu_table* gt, const uint8_t* in, uint64_t in_l
     if (st) return st;
     if (n) HIP_TRY(hipMemcpy(out, d_out.p, n * sym_bytes, hipMemcpyDeviceToHost));
     return ANS_OK;
-}
+} ANS_CATCH
 
 int ans_gpu_decode_chunks(ans_gpu_table* gt, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                           const uint64_t* lens, uint64_t n, uint64_t chunk_len, int gen_kind, void* out,
-                          int sym_bytes) {
+                          int sym_bytes) try {
     if (gen_kind != ANS_GEN_ZEROS && gen_kind != ANS_GEN_EMPTY) return ANS_E_ARG;  // RANDOM needs a seed: _ex
     return ans_gpu_decode_chunks_ex(gt, in, in_len, offsets, lens, n, chunk_len, gen_kind, 0, out, sym_bytes);
-}
+} ANS_CATCH
 
 }  // extern "C"

@@ -325,6 +325,15 @@ bool staged_decode_ok(const ans_gpu_table* gt) {  // large-alphabet or LDS-bucke
     return gt->ft.usable && ((sizeof(Sym) > 1 && gt->ft.dec_wide) || gt->ft.dec_usable);
 }
 
+// go(integral_constant<int, table's norm range>) for the large-alphabet kernels' kNR
+template <typename Go>
+void with_norm_range(const FastTable& ft, Go&& go) {
+    using std::integral_constant;
+    if (ft.nr == fast::kNormSmall) go(integral_constant<int, fast::kNormSmall>{});
+    else if (ft.nr == fast::kNormBig) go(integral_constant<int, fast::kNormBig>{});
+    else go(integral_constant<int, fast::kNormStd>{});
+}
+
 template <typename Sym>
 int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span, uint64_t nchunks, uint64_t lmax,
                          uint8_t* d_slots, uint64_t slot_cap, uint32_t* d_lens, uint32_t* d_status, hipStream_t s,
@@ -352,9 +361,11 @@ int launch_staged_encode(ans_gpu_table* gt, const Sym* syms, ChunkSpan<Sym> span
         if constexpr (sizeof(Sym) > 1) wide = ft.enc_wide;
         if (wide) {
             if constexpr (sizeof(Sym) > 1) {
-#define ENCV2(K32, PK, SA) fast::k_encode_w<Sym, K32, PK, SA, true><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
-#define ENCV(K32) if (ft.enc_sa) ENCV2(K32, true, true); else if (ft.enc_pack) ENCV2(K32, true, false); else ENCV2(K32, false, false)
-            if (k32) ENCV(true); else ENCV(false);
+#define ENCV2(K32, PK, SA, NR) fast::k_encode_w<Sym, K32, PK, SA, true, NR><<<grid, fast::kBlock, wlds, s>>>(ft, stage, lpad, nchunks, d_slots, slot_cap, d_lens, d_status, ini, vlen)
+#define ENCV(K32, NR) if (ft.enc_sa) ENCV2(K32, true, true, NR); else if (ft.enc_pack) ENCV2(K32, true, false, NR); else ENCV2(K32, false, false, NR)
+            if (ft.nr == fast::kNormBig) ENCV(true, fast::kNormBig);  // (K < 2^25)
+            else if (k32) ENCV(true, fast::kNormStd);
+            else ENCV(false, fast::kNormStd);
 #undef ENCV
 #undef ENCV2
             }
@@ -455,13 +466,16 @@ int launch_staged_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t*
         if (wide) {
           if constexpr (sizeof(Sym) > 1) {
             const unsigned wgrid = static_cast<unsigned>((nchunks + fast::kWideDecLanes - 1) / fast::kWideDecLanes);
-            if (ft.dec_c) {
-                FastTable fw = ft;
-                const size_t wl = wide_dec_lds(fw, wgrid, gt->g->ncu);
-                fast::k_decode_w<Sym, true, false, true><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
-            } else {
-                fast::k_decode_w<Sym, false, true, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
-            }
+            with_norm_range(ft, [&](auto nr) {
+                constexpr int NR = decltype(nr)::value;
+                if (ft.dec_c) {
+                    FastTable fw = ft;
+                    const size_t wl = wide_dec_lds(fw, wgrid, gt->g->ncu);
+                    fast::k_decode_w<Sym, true, false, true, false, NR><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+                } else {
+                    fast::k_decode_w<Sym, false, true, true, false, NR><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, lpad, nchunks, gen_kind, stage, d_status, ini, vlen);
+                }
+            });
           }
         } else {  // LDS buckets (ans_fast.hpp k_decode, kVar)
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;
@@ -489,6 +503,8 @@ uint64_t fast_chunks(const ans_gpu_table* gt, uint64_t n, uint64_t chunk_len, bo
     // of at most 2^24 symbols (4 bytes per push at most)
     if (decode && chunk_len > (1ull << 24)) return 0;
     if (decode ? !gt->ft.dec_usable : (sizeof(Sym) == 1 && gt->ft.enc_global)) return 0;
+    // kNormBig large alphabets encode on k_encode_w alone (128-B symbol groups)
+    if (!decode && gt->ft.enc_global && gt->ft.nr == fast::kNormBig && (chunk_len * sizeof(Sym)) % 128 != 0) return 0;
     return n / chunk_len;
 }
 
@@ -523,8 +539,8 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
                              else fast::k_encode<Sym, KM, K32, G><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini); } while (0)
 #define ENCN(KM, K32, NR) fast::k_encode<Sym, KM, K32, false, false, NR><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
 #define ENC_KMAX(G)                                                   \
-        if (!(G) && ft.nr == fast::kNormSmall) {                      \
-            ENCN(2, false, fast::kNormSmall);                         \
+        if (ft.nr == fast::kNormSmall) {  /* (kmax <= 2, K >= 2^40) */ \
+            fast::k_encode<Sym, 2, false, G, false, fast::kNormSmall><<<grid, fast::kBlock, lds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini); \
         } else if (!(G) && ft.nr == fast::kNormBig) {                 \
             switch (ft.kmax) {                                        \
             case 1: case 2: ENCN(2, true, fast::kNormBig); break;     \
@@ -541,9 +557,11 @@ int launch_encode(ans_gpu_table* gt, const void* d_syms, uint64_t n, uint64_t ch
         if constexpr (sizeof(Sym) > 1) {
             if (ft.enc_wide && (chunk_len * sizeof(Sym)) % 128 == 0) {
                 const size_t wlds = wide_enc_lds(ft);
-#define ENCW2(K32, PK, SA) fast::k_encode_w<Sym, K32, PK, SA><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
-#define ENCW(K32) if (ft.enc_sa) ENCW2(K32, true, true); else if (ft.enc_pack) ENCW2(K32, true, false); else ENCW2(K32, false, false)
-                if (k32) ENCW(true); else ENCW(false);
+#define ENCW2(K32, PK, SA, NR) fast::k_encode_w<Sym, K32, PK, SA, false, NR><<<grid, fast::kBlock, wlds, s>>>(ft, syms, chunk_len, nfull, d_slots, slot_cap, d_lens, d_status, ini)
+#define ENCW(K32, NR) if (ft.enc_sa) ENCW2(K32, true, true, NR); else if (ft.enc_pack) ENCW2(K32, true, false, NR); else ENCW2(K32, false, false, NR)
+                if (ft.nr == fast::kNormBig) ENCW(true, fast::kNormBig);  // (K < 2^25)
+                else if (k32) ENCW(true, fast::kNormStd);
+                else ENCW(false, fast::kNormStd);
 #undef ENCW
 #undef ENCW2
             } else if (ft.enc_global) {
@@ -604,18 +622,25 @@ int launch_decode(ans_gpu_table* gt, const uint8_t* d_in, const uint64_t* d_offs
                 // SIMD wait on an L2 round trip every step whatever the prefix covers, and the
                 // prefix path's VALU sat on that chain); the first buckets staged in the LDS the
                 // ring leaves (wide_dec_lds: one workgroup per CU)
-                if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0) {
-                    FastTable fw = ft;
-                    const size_t wl = wide_dec_lds(fw, wgrid, gt->g->ncu);
-                    if (ft.pmax < (1u << 24))
-                        fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
-                    else
-                        fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
-                }
-                else if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0)
-                    fast::k_decode_w<Sym, false, true><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
-                else
-                    fast::k_decode_g<Sym><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                with_norm_range(ft, [&](auto nr) {
+                    constexpr int NR = decltype(nr)::value;
+                    if (ft.dec_wide && ft.dec_c && (chunk_len * sizeof(Sym)) % 64 == 0) {
+                        FastTable fw = ft;
+                        const size_t wl = wide_dec_lds(fw, wgrid, gt->g->ncu);
+                        if constexpr (NR == fast::kNormStd) {
+                            if (ft.p24)
+                                fast::k_decode_w<Sym, true, false, false, true><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                            else
+                                fast::k_decode_w<Sym, true, false><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                        } else {
+                            fast::k_decode_w<Sym, true, false, false, false, NR><<<wgrid, fast::kWideDecLanes, wl, s>>>(fw, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                        }
+                    } else if (ft.dec_wide && (chunk_len * sizeof(Sym)) % 64 == 0) {
+                        fast::k_decode_w<Sym, false, true, false, false, NR><<<wgrid, fast::kWideDecLanes, 160 * 1024, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                    } else {
+                        fast::k_decode_g<Sym, NR><<<grid, fast::kBlock, fast::kDecGRingBytes, s>>>(ft, d_in, slot_cap, d_offsets, d_lens, chunk_len, nfull, gen_kind, out, d_status, ini);
+                    }
+                });
             }
         } else {
             const size_t lds = fast::kDecTableBytes + fast::kDecRingBytes;

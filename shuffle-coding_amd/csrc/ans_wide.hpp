@@ -95,12 +95,17 @@ __device__ __forceinline__ double rcp_newton(uint32_t p) {
 // partial, and it is the first one coded, so the pushes past vlen[c] are skipped there.
 // (A push emits at most 4 bytes whatever the table, and the renorm never loops over j, so the
 // kernel has no KMAX parameter: one unit of 8 u16 / 4 u32 symbols completes at most one page.)
-template <typename Sym, bool kK32, bool kPack, bool kSa, bool kVar = false>
+// kNR: kNormStd, or kNormBig (2^31 < norm < 2^32: a mass may reach 2^31, where the 32-bit
+// remainder test cannot tell r - p from r, so those rows always take the exact 64-bit branch, as
+// in ans_fast.hpp push_one; the quotient is below 2^33 there, so the estimate is as tight).
+// kNormSmall tables never come here (norm < 2^16 < kWideNormMin).
+template <typename Sym, bool kK32, bool kPack, bool kSa, bool kVar = false, int kNR = kNormStd>
 __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* __restrict__ syms, uint64_t chunk_len,
                                                          uint64_t nfull, uint8_t* __restrict__ slots, uint64_t slot_cap,
                                                          uint32_t* __restrict__ lens, uint32_t* __restrict__ status,
                                                          ChunkInit ini, const uint32_t* __restrict__ vlen = nullptr) {
     static_assert(!kSa || kPack, "the shift table comes with the packed prefix");
+    static_assert(kNR != kNormSmall, "norm < 2^16: the global-row k_encode");
     using Lay = WideEncLds<kSa, kPack>;
     extern __shared__ __align__(16) unsigned char lds[];
     {
@@ -262,11 +267,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             // q + 1.  The estimate from below (qest_m1) needed a borrow-select on every push.
             uint64_t qb = qest_half(head, rcp_newton(p));
             uint32_t rm = lo32(head) - lo32(qb) * p;
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(rm >= p) != 0, 0)) {
-                if (rm >= p) {  // a zero-mass push (p = 0: rm >= 0 = p) always lands here
+            const bool fix = kNR == kNormBig ? (rm >= p || static_cast<int32_t>(p) < 0) : rm >= p;
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(fix) != 0, 0)) {
+                if (fix) {  // a zero-mass push (p = 0: rm >= 0 = p) always lands here
                     minmass = min(minmass, p);
                     const int64_t r = static_cast<int64_t>(head - (qb - 0x4330000000000000ull) * p);
-                    const int64_t d = r < 0 ? -1 : 1;
+                    // (kNormBig's forced rows may be right already)
+                    const int64_t d = r < 0 ? -1 : (kNR != kNormBig || r >= static_cast<int64_t>(p) ? 1 : 0);
                     qb += static_cast<uint64_t>(d);
                     rm = static_cast<uint32_t>(r - d * static_cast<int64_t>(p));
                 }
@@ -485,15 +492,17 @@ struct DecChainW {
             if (!(low & 1)) fetch_pair((low >> 1) - 1);  // the next page (low-1, odd) opens a new pair
         }
     }
-    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm) {
+    template <int kNR = kNormStd>
+    __device__ __forceinline__ void renorm_div(uint64_t L, uint32_t hL8, uint32_t norm, double rcp_norm,
+                                               double neg_norm = 0.0) {
         form_window();
         P -= static_cast<int32_t>(renorm_up(head, W, L, hL8));
         read_window();  // for the next step; kept ahead of this step's lookups
         __builtin_amdgcn_sched_barrier(0);
-        div_norm(head, norm, rcp_norm, qq, cf);
+        div_norm<kNR>(head, norm, rcp_norm, qq, cf, neg_norm);
     }
     // head = p*q + r; with every mass below 2^24 (kP24) the high word's product is one
-    // v_mad_u32_u24 (hi32(q) < 2^16 for norm >= 2^16), as in ans_fast.hpp DecChain::update
+    // v_mad_u32_u24 (hi32(q) < 2^24 for norm > 256), as in ans_fast.hpp DecChain::update
     template <bool kP24>
     __device__ __forceinline__ void update(uint32_t p, uint32_t r) {
         if constexpr (kP24) {
@@ -513,8 +522,10 @@ struct DecChainW {
 // which for C4 is nearly every step, so the prefix only added VALU to the chain).
 // kVar: chunk c decodes vlen[c] <= chunk_len symbols into the start of its chunk_len-symbol
 // stride (staged output: the rest of its last 128-B line is garbage).
-// kP24: every mass is below 2^24 (DecChainW::update).
-template <typename Sym, bool kCompact, bool kPrefix, bool kVar = false, bool kP24 = false>
+// kP24: every mass is below 2^24 and the norm above 256 (DecChainW::update: hi32(q) < 2^24).
+// kNR: the norm range of div_norm (kNormSmall: more than 256 symbols below 2^16, a count-built
+// label table; kNormBig: 2^31 < norm < 2^32).
+template <typename Sym, bool kCompact, bool kPrefix, bool kVar = false, bool kP24 = false, int kNR = kNormStd>
 __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, const uint8_t* __restrict__ slots,
                                                          uint64_t slot_cap, const uint64_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ lens,
@@ -573,7 +584,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
         // the chain's part up to the bucket loads at raised wave priority (ans_fast.hpp k_decode;
         // decode -1.4% in a same-box A/B)
         __builtin_amdgcn_s_setprio(2);
-        ch.renorm_div(L, hL8, norm, rcp_norm);
+        ch.template renorm_div<kNR>(L, hL8, norm, rcp_norm, -static_cast<double>(norm));
         const uint32_t cf = ch.cf;
         const bool pre = kPrefix && cf < cpre;
         // global bucket (lanes past the prefix only): issued first, the longer round trip

@@ -5,9 +5,10 @@ The reference builds its dataset-level tables from counts: the edge Bernoulli
 `Bernoulli::new(total_edges, total_possible_edges)` and the node / edge label Categoricals
 (src/benchmark.rs:549-578), `Bernoulli::new(1, 2)` for the loops flag (src/param_codec.rs:273).
 Ordinary datasets give norms below 2^16; very large ones can pass 2^31.  Those tables used to
-take the one-lane generic kernels; every table here must now report the LDS fast paths and code
-every chunk to the oracle's bytes (fixed chunks, ragged chunks through the staged kernels,
-variable-length chunks, Message::random initial messages).
+take the one-lane generic kernels; every table here must now report the LDS fast paths (or, above
+256 symbols, the large-alphabet ones) and code every chunk to the oracle's bytes (fixed chunks,
+ragged chunks through the staged kernels, variable-length chunks, Message::random initial
+messages).
 """
 import numpy as np
 import pytest
@@ -148,32 +149,76 @@ def test_norm_range_var_chunks(gpu, name):
 
 @pytest.mark.parametrize("name", ["c3_small", "c3_big"])
 def test_norm_range_whole_gib(gpu, name):
-    """bench.py's c3s / c3b workloads (2^30 u8 symbols, chunk 4096) on the device: every chunk
-    length equals the oracle's (chunk-parallel oracle encode of the same counter-based symbols)
-    and the round trip is lossless."""
-    torch = pytest.importorskip("torch")
-    masses = _table(name)
+    """bench.py's c3s / c3b workloads (2^30 u8 symbols, chunk 4096) on the device, byte-checked
+    like C3 itself (test_gpu_parity._device_roundtrip): every one of the 262,144 chunks' lengths,
+    and the bytes of the whole dense container as a sha256 per slice of chunks against the
+    oracle's streams of the same counter-based symbols; the round trip is lossless from the slots
+    and from the dense container."""
+    from test_gpu_parity import _device_roundtrip
+    total = _device_roundtrip(gpu, _table(name), 1 << 30, 4096, 1, 1)
+    assert 0.9 < total / (1 << 30) < 1.0
+
+
+# ---- more than 256 symbols outside [2^16, 2^31]: the large-alphabet kernels' kNormSmall /
+# kNormBig division (ans_fast.hpp k_encode with global rows and k_decode_g, ans_wide.hpp
+# k_encode_w / k_decode_w with kNR; DESIGN.md §4b)
+def _label_counts(rng, nsym, total):
+    """A count-built label Categorical (DatasetStats::dist, src/benchmark.rs:576-578): Zipf-like
+    counts over nsym labels, some labels absent (zero mass), summing to about `total`."""
+    w = 1.0 / np.arange(1, nsym + 1) ** 0.9
+    c = np.floor(w / w.sum() * total).astype(np.int64)
+    c[rng.choice(nsym, size=nsym // 10, replace=False)] = 0
+    c[0] = max(c[0], 1)
+    return c.astype(np.uint64)
+
+
+WIDE = {
+    # kNormSmall
+    "labels_4096_norm_6e4": lambda r: _label_counts(r, 4096, 60000),
+    "wide_300_norm_1000": lambda r: _spread(r, 300, 1000),
+    "wide_65536_ones": lambda r: np.ones(65535, np.uint64),  # norm 2^16 - 1, every mass 1
+    # kNormBig
+    "wide_1000_norm_2^32-5": lambda r: _spread(r, 1000, (1 << 32) - 5),
+    "wide_65536_mass_above_2^31": lambda r: np.concatenate([[(1 << 31) + 999], r.integers(1, 1 << 14, 65535)]).astype(
+        np.uint64),
+}
+
+
+def _wide(name):
+    masses = WIDE[name](np.random.default_rng(sum(map(ord, name))))
+    norm = int(masses.sum())
+    assert len(masses) > 256 and (norm < (1 << 16) or (1 << 31) < norm < (1 << 32)), norm
+    return masses
+
+
+@pytest.mark.parametrize("name", sorted(WIDE))
+def test_wide_norm_range_tables_take_the_fast_kernels(gpu, name):
+    masses = _wide(name)
     gt = A.GpuTable(gpu, A.Categorical(masses))
-    n, L = 1 << 30, 4096
-    stream = torch.cuda.Stream()
-    syms = torch.empty(n, dtype=torch.uint8, device="cuda")
-    gt.dev_gen_iid(1, 0, n, syms, 1, stream)
-    cap = gt.slot_capacity(L)
-    slots = torch.empty((n // L) * cap, dtype=torch.uint8, device="cuda")
-    lens = torch.zeros(n // L, dtype=torch.int32, device="cuda")
-    status = torch.zeros(1, dtype=torch.int32, device="cuda")
-    gt.dev_encode(syms, 1, n, L, slots, cap, lens, status, stream)
-    out = torch.empty_like(syms)
-    gt.dev_decode(slots, None, cap, lens, n, L, out, 1, status, stream)
-    assert gpu.status(status, stream) == 0
-    assert torch.equal(out, syms)
-    lh = lens.cpu().numpy().astype(np.uint64)
-    host = syms.cpu().numpy()
-    del slots, out
-    from concurrent.futures import ThreadPoolExecutor
-    parts = 16
-    step = n // parts
-    with ThreadPoolExecutor(8) as ex:
-        ol = list(ex.map(lambda i: orc.encode_chunks(masses, host[i * step:(i + 1) * step].astype(np.uint32), L)[2],
-                         range(parts)))
-    assert np.array_equal(lh, np.concatenate(ol))
+    p = gt.paths()
+    assert p & (A.ANS_PATH_ENC_GLOBAL | A.ANS_PATH_ENC_WIDE), hex(p)
+    assert p & (A.ANS_PATH_DEC_GLOBAL | A.ANS_PATH_DEC_WIDE), hex(p)
+    n = 300 * 4096 + 77  # full chunks on the fast kernels, the ragged last one generic
+    syms = _symbols(masses, n, 3)
+    for dtype in (np.uint16, np.uint32):
+        _roundtrip(gt, masses, syms, 4096, dtype)
+    _roundtrip(gt, masses, syms[:200 * 1563 + 5], 1563, np.uint16)  # staged (ragged) chunks
+    _roundtrip(gt, masses, syms[:520 * 4096], 4096, np.uint16, gen_kind=A.GEN_RANDOM, seed=4)
+
+
+@pytest.mark.parametrize("name", ["labels_4096_norm_6e4", "wide_65536_mass_above_2^31"])
+def test_wide_norm_range_var_chunks(gpu, name):
+    masses = _wide(name)
+    rng = np.random.default_rng(17)
+    sizes = np.concatenate([[0, 1, 7], rng.integers(0, 2500, 300), [9000, 0]]).astype(np.uint64)
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    syms = _symbols(masses, int(starts[-1]), 19).astype(np.uint16)
+    gt = A.GpuTable(gpu, A.Categorical(masses))
+    data, offsets, lens = gt.encode_var_chunks(syms, starts)
+    for c in range(len(sizes)):
+        a, b = int(starts[c]), int(starts[c + 1])
+        od, _, _ = orc.encode_chunks(masses, syms[a:b].astype(np.uint32), max(b - a, 1))
+        want = od.tobytes() if b > a else bytes(orc.Message.zeros().flatten())
+        assert data[int(offsets[c]):int(offsets[c] + lens[c])].tobytes() == want, c
+    back = gt.decode_var_chunks(data, offsets, lens, starts, np.uint16)
+    assert np.array_equal(back, syms)

@@ -77,7 +77,7 @@ def _random_case(rng, nsym, lo, hi, zero_frac, n):
     (1024, 1 << 10, 1 << 21, 0.0, 1, 3000),     # one symbol per chunk
     (4096, 1, 1 << 12, 0.0, 999, 200_000),      # LDS-sized large alphabet
     (65536, 1, 1 << 12, 0.0, 4096, 400_000),    # C4 alphabet: table from global memory
-    (300, 1 << 22, 1 << 24, 0.0, 512, 50_000),  # norm > 2^31: generic path
+    (300, 1 << 22, 1 << 24, 0.0, 512, 50_000),  # norm > 2^31: the wide kNormBig kernels
     (3, 1, 2, 0.0, 100, 1000),                  # norm 3..6
     # fast-kernel shapes (chunk_len * width a multiple of 16, >= 512 chunks, ragged tail)
     (256, 1, 1 << 20, 0.0, 64, 100_003),

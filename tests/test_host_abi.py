@@ -48,6 +48,47 @@ def test_no_gpu_here_fails_loudly():
     assert e.value.code == A.ANS_E_DEVICE
 
 
+def test_gpu_entry_allocation_failure_is_a_status():
+    """SURVEY.md §8b: no exception crosses the ABI.  ans_gpu_graphs_decode sizes a std::vector by
+    num_graphs before any device call; 2^62 entries exceed std::vector's max_size, so it throws
+    std::length_error -- the entry's function-try-block returns ANS_E_ALLOC instead of aborting
+    the (ctypes) caller.  No GPU and no real handle is needed to reach it."""
+    L = A.lib()
+    dummy = ctypes.create_string_buffer(64)  # never dereferenced before the throw
+    nn = np.zeros(4, np.uint32)
+    offs, lens, eo = np.zeros(4, np.uint64), np.zeros(4, np.uint64), np.zeros(4, np.uint64)
+    rc = L.ans_gpu_graphs_decode(ctypes.cast(dummy, ctypes.c_void_p), A.ANS_NO_TABLE, A.ANS_NO_TABLE, 0, 0, 0, 1 << 62,
+                                 A._np_ptr(nn), None, 0, A._np_ptr(offs), A._np_ptr(lens), A.GEN_ZEROS, 0, None, None,
+                                 None, 0, A._np_ptr(eo))
+    assert rc == A.ANS_E_ALLOC
+
+
+def test_every_gpu_entry_is_exception_guarded():
+    """Every extern "C" definition of the HIP units is a function-try-block ending in ANS_CATCH
+    (shuffle-coding_amd/csrc/ans_ctx.hpp), except one-line bodies that cannot throw."""
+    csrc = os.path.join(ROOT, "shuffle-coding_amd", "csrc")
+    unguarded = []
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith(".hip"):
+            continue
+        text = open(os.path.join(csrc, fn)).read()
+        n_defs = 0
+        for block in re.findall(r'^extern "C" \{\n(.*?)^\}  // extern "C"', text, flags=re.S | re.M):
+            lines = block.split("\n")
+            for i, line in enumerate(lines):
+                m = re.match(r"(?:int|void|uint64_t) ((?:ans|dev)_\w+)\(", line)
+                if not m or line.rstrip().endswith("}"):  # (a declaration-free one-liner)
+                    continue
+                n_defs += 1
+                j = next(k for k in range(i, len(lines)) if lines[k].rstrip().endswith("{"))
+                end = next(k for k in range(j + 1, len(lines)) if lines[k].startswith("}"))
+                if not (lines[j].rstrip().endswith(") try {") and lines[end].startswith("} ANS_CATCH")):
+                    unguarded.append(f"{fn}:{m.group(1)}")
+        if fn in ("ans_kernels.hip", "ans_codecs.hip", "ans_graph.hip"):
+            assert n_defs >= 9, fn
+    assert not unguarded, unguarded
+
+
 def test_multiset_single_message_matches_golden(multiset_masses, multiset_vectors, golden_multiset):
     cat = A.Categorical(multiset_masses)
     for size, syms in multiset_vectors.items():
