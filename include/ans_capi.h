@@ -9,7 +9,10 @@
  *
  * Threading: a Message handle is single-threaded (the reference's `&mut Message`);
  * tables are immutable after creation and may be shared; GPU handles are per device,
- * one HIP stream each, and must not be used from two threads at once.
+ * one HIP stream each, and must not be used from two threads at once.  A GPU table or
+ * table set may be freed before or after its context (the free touches only the table,
+ * e.g. from a garbage collector that finalizes both in any order); every other call on it
+ * needs its context alive.
  */
 #ifndef ANS_CAPI_H
 #define ANS_CAPI_H

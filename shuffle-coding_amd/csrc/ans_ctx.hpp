@@ -60,6 +60,7 @@ struct ans_gpu {
 
 struct ans_gpu_table {
     ans_gpu* g;
+    int device;          // g->device, kept here: freeing the table never touches its context
     DevTable t;
     void* d_mem;
     uint32_t lds_bytes;  // 0 = table read from global memory (L2-resident)

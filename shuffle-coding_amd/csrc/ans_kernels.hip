@@ -1333,7 +1333,7 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
         if (rc) return rc;
         DevTable t{};
         t.nsym = nsym > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(nsym);
-        auto* gt = new (std::nothrow) ans_gpu_table{g, t, nullptr, 0, FastTable{}, nullptr, ts};
+        auto* gt = new (std::nothrow) ans_gpu_table{g, g->device, t, nullptr, 0, FastTable{}, nullptr, ts};
         if (!gt) {
             ans_tableset_destroy(ts);
             return ANS_E_ALLOC;
@@ -1374,7 +1374,7 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
     HIP_TRY(hipMemcpy(static_cast<char*>(mem) + rows_bytes, buckets.data(), bucket_bytes, hipMemcpyHostToDevice));
     t.sym = static_cast<const DevSym*>(mem);
     t.bucket = reinterpret_cast<const uint16_t*>(static_cast<char*>(mem) + rows_bytes);
-    auto* gt = new (std::nothrow) ans_gpu_table{g, t, mem, 0, FastTable{}, nullptr, nullptr};
+    auto* gt = new (std::nothrow) ans_gpu_table{g, g->device, t, mem, 0, FastTable{}, nullptr, nullptr};
     if (!gt) { (void)hipFree(mem); return ANS_E_ALLOC; }
     if (rows_bytes + bucket_bytes <= kLdsTableLimit) gt->lds_bytes = static_cast<uint32_t>(rows_bytes + bucket_bytes);
     const int rc = build_fast_table(gt, cat);
@@ -1388,7 +1388,7 @@ int ans_gpu_table_create(ans_gpu* g, const ans_table* tab, ans_gpu_table** out) 
 
 void ans_gpu_table_free(ans_gpu_table* gt) try {
     if (!gt) return;
-    (void)hipSetDevice(gt->g->device);
+    (void)hipSetDevice(gt->device);  // (not gt->g: a table may be freed after its context)
     if (gt->ts64) ans_tableset_destroy(gt->ts64);
     if (gt->d_mem) (void)hipFree(gt->d_mem);
     if (gt->d_fast) (void)hipFree(gt->d_fast);

@@ -146,17 +146,21 @@ def _big_norm_tables(rng):
     return t
 
 
+@pytest.mark.parametrize("lanes", [256, 1024])
 @pytest.mark.parametrize("which", ["small", "big"])
 @pytest.mark.parametrize("dtype,L", [(np.uint8, 4096), (np.uint8, 128), (np.uint16, 512)])
-def test_independent_fast_norm_ranges(gpu, which, dtype, L):
+def test_independent_fast_norm_ranges(gpu, which, dtype, L, lanes):
     """Sets whose norms all lie below 2^16 (or all in (2^31, 2^32)) take the fast kernels with
-    the long-division (64-bit-checked) quotient of ans_fast.hpp kNormSmall (kNormBig)."""
+    the long-division (64-bit-checked) quotient of ans_fast.hpp kNormSmall (kNormBig), in both
+    workgroup layouts: 256 lanes (what dataset-sized calls take by default) and 1,024 lanes
+    sharing one LDS image (the big set's decoder image does not fit 28 KiB: its decodes stay on
+    256 lanes there)."""
     rng = np.random.default_rng(300 + L + len(which))
     tables = _small_norm_tables(rng) if which == "small" else _big_norm_tables(rng)
     for m in tables:
         assert (int(m.sum()) < 1 << 16) if which == "small" else ((1 << 31) < int(m.sum()) < (1 << 32))
     ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
-    ts.lanes(1024)  # (the big set's decoder buckets need more than 28 KiB: its encoder alone)
+    ts.lanes(lanes)
     assert ts.fast() in (1, 2)
     n = 301 * L + 17
     tids = rng.integers(0, len(tables), size=n).astype(np.uint32)
@@ -164,7 +168,7 @@ def test_independent_fast_norm_ranges(gpu, which, dtype, L):
     for t, m in enumerate(tables):  # uniform over each table's symbols: the rare rows often
         sel = tids == t
         syms[sel] = rng.choice(np.flatnonzero(m), size=int(sel.sum()))
-    for kind, seed in [(A.GEN_ZEROS, 0), (A.GEN_RANDOM, 4)]:
+    for kind, seed in [(A.GEN_ZEROS, 0), (A.GEN_RANDOM, 4), (A.GEN_EMPTY, 0)]:
         _check_indep(ts, tables, tids, syms, L, dtype, kind, seed)
 
 
@@ -273,6 +277,41 @@ def test_independent_fast_device_api_dense(gpu):
     d_offs = torch.from_numpy(oo.astype(np.int64)).cuda()
     out = torch.zeros_like(d_syms)
     ts.dev_decode(d_tids, d_dense, d_offs, cap, lens, n, L, out, 1, status, stream, A.GEN_RANDOM, 3)
+    assert gpu.status(status, stream) == 0
+    assert torch.equal(out, d_syms)
+
+
+@pytest.mark.parametrize("offsets", [(1, 0, 0), (0, 3, 0), (0, 0, 8), (5, 7, 4)])
+def test_independent_misaligned_device_buffers(gpu, offsets):
+    """ans_dev_independent_*: the fast kernels move symbols, table ids and slot pages with 16-B
+    vector accesses; views offset from 16-B alignment (symbols, ids, slots) take the exact kernels
+    and code the same bytes."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(9)
+    tables = _fast_tables(rng)
+    ts = A.GpuTableSet(gpu, [A.Categorical(m) for m in tables])
+    L, nchunks = 1024, 64
+    n = L * nchunks
+    tids, syms = _indep_case(rng, tables, n)
+    os_, ot, ob = offsets
+    stream = torch.cuda.Stream()
+    d_syms = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")[os_:os_ + n]
+    d_syms.copy_(torch.from_numpy(syms.astype(np.uint8)))
+    d_tids = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")[ot:ot + n]
+    d_tids.copy_(torch.from_numpy(tids.astype(np.uint8)))
+    cap = ts.slot_capacity(L)
+    slots = torch.zeros(nchunks * cap + 16, dtype=torch.uint8, device="cuda")[ob:ob + nchunks * cap]
+    lens = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ts.dev_encode(d_tids, d_syms, 1, n, L, slots, cap, lens, status, stream)
+    assert gpu.status(status, stream) == 0
+    od, oo, ol = orc.codec_encode_chunks(orc.CODEC_INDEPENDENT, syms, L, tables=tables, tids=tids)
+    ln = lens.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(ln, ol)
+    sl = slots.cpu().numpy().reshape(nchunks, cap)
+    assert np.concatenate([sl[c, :ln[c]] for c in range(nchunks)]).tobytes() == od.tobytes()
+    out = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")[os_:os_ + n]
+    ts.dev_decode(d_tids, slots, None, cap, lens, n, L, out, 1, status, stream)
     assert gpu.status(status, stream) == 0
     assert torch.equal(out, d_syms)
 

@@ -1002,7 +1002,24 @@ def _wide_rerun_masses():
     return m
 
 
-@pytest.mark.parametrize("which", ["c3_u8", "wide_u16"])
+def _norm255_masses():
+    """40 masses summing to 255 (kNormSmall at norm <= 256: the 24-bit high-word product off)."""
+    m = np.full(40, 6, np.int64)
+    m[:15] += 1
+    assert int(m.sum()) == 255
+    return m.astype(np.uint64)
+
+
+def _wide_small_masses():
+    """1,000 symbols below 2^16 (the wide decoder's kNormSmall long division) with large masses."""
+    rng = np.random.default_rng(6)
+    m = rng.integers(1, 40, 1000).astype(np.uint64)
+    m[[3, 500, 998]] = [9000, 6000, 5000]
+    assert int(m.sum()) < (1 << 16)
+    return m
+
+
+@pytest.mark.parametrize("which", ["c3_u8", "wide_u16", "c3_small_u8", "norm255_u8", "wide_small_u16"])
 def test_decoder_deferred_screen_reruns_the_unit(gpu, which):
     """The C3 decoder takes the renorm's one-byte-less screen once per unit (ans_fast.hpp
     k_decode kDefer) and re-runs a unit where a lane reached it; the large-alphabet decoder
@@ -1010,10 +1027,13 @@ def test_decoder_deferred_screen_reruns_the_unit(gpu, which):
     exactly L (inside the window [L, 2^56) where the clz rule pulls one byte too many) take
     that path; they sit in the same waves as ordinary chunks, and every chunk's symbols must
     equal the oracle's pops of the same stream (the crafted streams end in a mismatch status,
-    which the ordinary ones must not share)."""
+    which the ordinary ones must not share).  The kNormSmall tables (norm 32,749, norm 255, and
+    1,000 symbols below 2^16 on the wide decoder) take the same re-run through their long-division
+    quotient (ans_fast.hpp renorm_div_u's div_hi state)."""
     torch = pytest.importorskip("torch")
-    masses = A.c3_masses() if which == "c3_u8" else _wide_rerun_masses()
-    sym_bytes = 1 if which == "c3_u8" else 2
+    masses = {"c3_u8": A.c3_masses, "wide_u16": _wide_rerun_masses, "c3_small_u8": A.c3_small_masses,
+              "norm255_u8": _norm255_masses, "wide_small_u16": _wide_small_masses}[which]()
+    sym_bytes = 1 if which.endswith("u8") else 2
     norm = int(masses.sum())
     K = (1 << 56) // norm
     L = norm * K
@@ -1023,7 +1043,7 @@ def test_decoder_deferred_screen_reruns_the_unit(gpu, which):
     chunk_len, nch = 4096, 512
     rng = np.random.default_rng(77)
     gt = A.GpuTable(gpu, A.Categorical(masses))
-    assert gt.decode_kernel(sym_bytes) == ("lds" if which == "c3_u8" else "wide")
+    assert gt.decode_kernel(sym_bytes) == ("lds" if sym_bytes == 1 else "wide")
     cap = gt.slot_capacity(chunk_len)
     slots = np.zeros(nch * cap, np.uint8)
     lens = np.zeros(nch, np.uint32)
