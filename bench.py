@@ -53,6 +53,8 @@ CONFIGS = {
     "c3s": ("c3_small_masses", 30, 1, 1),  # ... to norm 32,749 (< 2^16: count-built dataset tables)
     "c3b": ("c3_big_masses", 30, 1, 1),  # ... to norm 2^32 - 5 (> 2^31)
     "c4": ("c4_masses", 29, 2, 2),
+    "c4s": ("c4_small_masses", 29, 2, 2),  # 4,096 of C4's masses quantised to norm 65,521 (< 2^16)
+    "c4b": ("c4_big_masses", 29, 2, 2),  # C4's table quantised to norm 2^32 - 5 (> 2^31)
 }
 
 

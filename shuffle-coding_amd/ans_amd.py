@@ -1398,6 +1398,17 @@ def c4_masses():
     return (np.uint64(1) + (splitmix64_np(np.uint64(0xC4) ^ s) & np.uint64((1 << 12) - 1))).astype(np.uint64)
 
 
+def c4_small_masses():
+    """The first 4,096 of C4's masses quantised to norm 65,521 (the largest prime below 2^16): a
+    large-alphabet table in the count-built norm range (src/benchmark.rs:576-578)."""
+    return quantise_masses(c4_masses()[:4096], 65521)
+
+
+def c4_big_masses():
+    """C4's 65,536 masses quantised to norm 4,294,967,291 (the largest prime below 2^32)."""
+    return quantise_masses(c4_masses(), 4294967291)
+
+
 def read_multiset(path):
     """The reference harness' reader (src/multiset.rs:161-166): ", "-separated integers."""
     with open(path) as f:
