@@ -639,7 +639,19 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_mdec(Model md, con
     // the table ids of a line (LU * U bytes, one u32 word per four ids) and of the next line,
     // whose load is issued at the line's first point: whole lines per load (r05: 16-B loads a
     // unit apart left each lane's id line to be evicted between them, 5.3 GB read per launch for
-    // 2.1 GB of stream and ids at 2^30 u8 symbols)
+    // 2.1 GB of stream and ids at 2^30 u8 symbols).
+    // r06, 1,024 lanes (kPair): with one 64-B id load per 64-B output line, a line ahead, each
+    // 128-B id line's second half came back from HBM 64 pops after its first (3.14 GB read per
+    // launch for 2.11 GB, profiles/r05t_codecs_pmc.json).  Now the two halves of a 128-B id line
+    // (the ids of lines 2m and 2m + 1) are fetched one unit (16 pops) apart: the even half in
+    // the last unit of line 2m - 1, the odd half at the first point of line 2m, so the line is
+    // still in L2 for the second.  The ids (< kIndMaxTables = 15 on these kernels: four bits) of
+    // both lines are held packed, even line in the low nibble of each byte, odd in the high one:
+    // each landed half is merged into its nibbles (two VALU per word, 1/4 VALU per pop for u8),
+    // 16 VGPRs for the pair as for one line before (holding a whole 128-B load spilled at 1,024
+    // lanes' 128 VGPRs), and a line's id is one v_bfe at nibble 4 * (line & 1).  (Not for
+    // kNormSmall sets, Model::kPairIds: their longer pop leaves no room for it, 12-20 B spilled.)
+    constexpr bool kPair = Model::kTids && kL == kLanesW && Model::kPairIds;
     constexpr int TW = LU * U / 4;  // u32 words of ids per line
     uint32_t tl[TW], tn[TW];
 #pragma unroll
@@ -655,11 +667,25 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_mdec(Model md, con
             w[4 * k + 3] = v.w;
         }
     };
+    auto merge_ids = [&](bool odd) __attribute__((always_inline)) {  // tn (landed) -> tl's nibbles
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+            if constexpr (kPair) {
+                uint32_t w;
+                if (odd) asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(w) : "v"(0xF0F0F0F0u), "v"(tn[k] << 4), "v"(tl[k]));
+                else asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(w) : "v"(0x0F0F0F0Fu), "v"(tn[k]), "v"(tl[k]));
+                tl[k] = w;
+            } else {
+                tl[k] = tn[k];
+            }
+        }
+    };
     if constexpr (Model::kTids) {
-        if (nunit > 0) load_ids(0, tl);
+        if (nunit > 0) load_ids(0, tn);
     }
     uint4 q[LU];
     for (int u0 = 0; u0 < nunit; u0 += LU) {
+        const uint32_t par = kPair ? static_cast<uint32_t>(u0 / LU) & 1u : 0u;  // (uniform) line parity
         auto unit = [&](auto ic) __attribute__((always_inline)) {
             constexpr int uu = decltype(ic)::value;
             uint4 outv = make_uint4(0, 0, 0, 0);
@@ -667,13 +693,24 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_mdec(Model md, con
             for (int j = 0; j < U; ++j) {
                 if (j % SPP == 0) {
                     wait_vm();  // point
+                    if constexpr (Model::kTids && !kPair) {
+                        if (j == 0 && uu == 0) {
+                            merge_ids(false);  // this line's ids (landed at this point)
+                            if (u0 + LU < nunit) load_ids(u0 / LU + 1, tn);  // the next line's
+                        }
+                    }
+                    if constexpr (kPair) {
+                        if (j == 0 && uu == 0 && par == 0) {
+                            merge_ids(false);             // line 2m's half (landed at this point)
+                            load_ids(u0 / LU + 1, tn);    // line 2m + 1's half, one unit later
+                        }
+                        if (j == 0 && uu == 1 && par == 0) merge_ids(true);
+                        if (j == 0 && uu == LU - 1 && par == 1 && u0 + LU < nunit) load_ids(u0 / LU + 1, tn);
+                    }
                     if (j == 0 && uu == 0 && u0 > 0) {
                         uint4* d = dst + (u0 - LU);
 #pragma unroll
                         for (int k = 0; k < LU; ++k) d[k] = q[k];
-                    }
-                    if constexpr (Model::kTids) {
-                        if (j == 0 && uu == 0 && u0 + LU < nunit) load_ids(u0 / LU + 1, tn);
                     }
                     ch.point();
                 }
@@ -681,7 +718,8 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_mdec(Model md, con
                 uint32_t tid = 0;
                 if constexpr (Model::kTids) {
                     const int tb = uu * U + j;  // id byte within the line (the pop fences the id)
-                    tid = (tl[tb / 4] >> (8 * (tb % 4))) & 0xFFu;
+                    if constexpr (kPair) tid = __builtin_amdgcn_ubfe(tl[tb / 4], 8 * (tb % 4) + 4 * par, 4);
+                    else tid = (tl[tb / 4] >> (8 * (tb % 4))) & 0xFFu;
                 }
                 uint32_t hi = 0;
                 uint32_t lo = md.pop(ch, ds, tid, hi);
@@ -696,10 +734,6 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_mdec(Model md, con
             q[uu] = outv;
         };
         unroll_seq(unit, std::make_integer_sequence<int, LU>{});
-        if constexpr (Model::kTids) {
-#pragma unroll
-            for (int k = 0; k < TW; ++k) tl[k] = tn[k];
-        }
     }
     wait_vm();
     if (nunit > 0) {  // the last line (nunit is a multiple of 8: chunk bytes % 128 == 0)
@@ -794,6 +828,7 @@ template <bool kRare, int kNR = fast::kNormStd, uint32_t kTabD = kDecTab, bool k
           uint32_t kTabEnc = kEncTab>
 struct IndepModel {
     static constexpr bool kTids = true;
+    static constexpr bool kPairIds = kNR != fast::kNormSmall;  // k_mdec's paired id halves (1,024 lanes)
     static constexpr uint32_t kTab = kTabD;
     static constexpr uint32_t kTabE = kTabEnc;
     using DecState = NoState;
@@ -993,6 +1028,7 @@ struct IndepModel {
 template <bool kPow2>
 struct UniformModel {
     static constexpr bool kTids = false;
+    static constexpr bool kPairIds = false;
     static constexpr uint32_t kTab = kDecTab;
     static constexpr uint32_t kTabE = kEncTab;
     using DecState = NoState;
@@ -1042,6 +1078,7 @@ struct LogUniformState {
 };
 struct LogUniformModel {
     static constexpr bool kTids = false;
+    static constexpr bool kPairIds = false;
     static constexpr uint32_t kTab = kDecTab;
     static constexpr uint32_t kTabE = kEncTab;
     using DecState = LogUniformState;
