@@ -68,14 +68,18 @@ static_assert(kDecRowOff + 8 * 257 <= kDecTableBytes, "row decode tables fit");
 // v - 256 at norm + cdf(v - 256) (q = q_m + 1).  Buckets of u (width 2^us) as 8-B threshold
 // pairs, then 512 rows (cum_row, p) with head = p * q_m + (u - cum_row).  A bucket at a = j << us
 // holds, for its boundaries c = cdfv(s0+1) and cdfv(s0+2) (s0 = the virtual symbol at a), the
-// word ((min(c - a, 2^us) - 1) << (32 - us)) | s0: u's offset in the bucket shifted to the top,
-// rx = u << (32 - us), exceeds it exactly when u >= c (its low bits are zero, the word's are
-// s0), so s = s0 + [rx > w1] + [rx > w2] comes from two compares and two v_addc on w1 itself,
-// with no separate s0 array (one random LDS read fewer per symbol).  The bits of w1 above s0
-// start at bit 32 - us >= 13 and leave the row address ((s << 3) mod 2^16) alone: us <= 19.
+// word (j & 1) << 31 | ((min(c - a, 2^us) - 1) << (31 - us)) | s0: u's offset in the bucket
+// shifted up to bit 30 under the bucket index's low bit; rx = u << (31 - us) (mod 2^32) holds the
+// same bit 31 and exceeds the word exactly when u >= c (its low bits are zero, the word's are
+// s0).  The two differ by less than 2^31, so [rx > w] is the sign bit of w - rx, and
+// s = w1 + ((w1 - rx) >> 31) + ((w2 - rx) >> 31) in its low bits: two v_sub, two v_lshrrev and
+// a v_add3 (r06, 14.2 issue cycles; two v_cmp / v_addc pairs took 19.1 with their vcc hazards),
+// on w1 itself, with no separate s0 array (one random LDS read fewer per symbol).  The bits of
+// w1 above s0 start at bit 31 - us >= 13 and leave the row address ((s << 3) mod 2^16) alone:
+// us <= 18 (norm up to 3,072 * 2^17 = 402,653,184; wider tables keep the row decoder).
 constexpr uint32_t kDecUNbMax = (kDecTableBytes - 8 * 512) / 8;
 constexpr uint32_t kDecURowOff = 8 * kDecUNbMax;
-constexpr uint32_t kDecUShiftMax = 19;
+constexpr uint32_t kDecUShiftMax = 18;
 static_assert(kDecURowOff + 8 * 512 <= kDecTableBytes, "u-domain decode tables fit");
 static_assert(kDecURowOff <= 65535, "ds offsets");
 // decode lookup modes (k_decode kMode)
@@ -1042,22 +1046,17 @@ struct DecChain {
         else qq = mk64(hw - 0x43000000u, lo32(raw));   // q_m < 2^52 (+ qh 2^32)
     }
     // the u-domain icdf: bucket u >> shift -> threshold words (w1, w2) with s0 in w1's low bits
-    // (kDecUNbMax), the virtual symbol v = s0 + [rx > w1] + [rx > w2] for rx = u << rshift, then
-    // its row (cum_row, p); only v's low 13 bits reach the row address
+    // (kDecUNbMax), the virtual symbol v = s0 + [rx > w1] + [rx > w2] for rx = u << rshift
+    // (rshift = 31 - shift: rx and the words agree in bit 31, so each test is a sign bit), then its
+    // row (cum_row, p); only v's low 13 bits reach the row address
     __device__ __forceinline__ void lookup_u(uint32_t shift, uint32_t rshift) {
         const uint32_t bi = cf >> shift;
         const uint64_t cc = lds_ld64(shl16<3>(bi));  // bi < kDecUNbMax
         const uint32_t rx = cf << rshift;
-        asm volatile(
-            "v_cmp_gt_u32 vcc, %[rx], %[w1]\n\t"
-            "s_nop 1\n\t"
-            "v_addc_co_u32 %[sx], vcc, 0, %[w1], vcc\n\t"
-            "v_cmp_gt_u32 vcc, %[rx], %[w2]\n\t"
-            "s_nop 1\n\t"
-            "v_addc_co_u32 %[sx], vcc, 0, %[sx], vcc"
-            : [sx] "=&v"(sx)
-            : [rx] "v"(rx), [w1] "v"(lo32(cc)), [w2] "v"(hi32(cc))
-            : "vcc");
+        const uint32_t w1 = lo32(cc), w2 = hi32(cc);
+        asm volatile("v_add3_u32 %0, %1, %2, %3"
+                     : "=v"(sx)
+                     : "v"(w1), "v"((w1 - rx) >> 31), "v"((w2 - rx) >> 31));
         const uint64_t row = lds_ld64(kDecURowOff + shl16<3>(sx));  // (sx mod 2^13) < 512
         cum = lo32(row);
         nxt = hi32(row);  // pmf(s)
@@ -1275,7 +1274,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
                                 asm("v_max3_u32 %0, %1, %2, %3" : "=v"(hmax) : "v"(hmax), "v"(hodd), "v"(hi32(ch.head)));
                             }
                         }
-                        ch.lookup_u(shift, 32u - shift);
+                        ch.lookup_u(shift, 31u - shift);
                         __builtin_amdgcn_s_setprio(0);
                     } else {
                         ch.template renorm_div<kJ4, kNR>(L, hL8, norm, rcp_norm, neg_norm);
@@ -1300,7 +1299,7 @@ __global__ __launch_bounds__(kDecBlock, 4) void k_decode(FastTable t, const uint
 #pragma unroll
                         for (int j = 0; j < U; ++j) {
                             ch.template renorm_div_u<kJ4, kNR, kP24, true>(L, hL8, norm, rcp_norm, rcp8, magic_u, neg_norm);
-                            ch.lookup_u(shift, 32u - shift);
+                            ch.lookup_u(shift, 31u - shift);
                             ch.template update<kP24, kRows>();
                             sv[j] = ch.sx;
                             if constexpr (kPack4) {

@@ -357,16 +357,19 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
             }
             return lo;
         };
-        uint32_t us = 1;  // (rx = u << (32 - us) must stay a 32-bit shift)
+        uint32_t us = 1;  // (rx = u << (31 - us) must stay a 32-bit shift)
         while (((n2 - 1) >> us) + 1 > fast::kDecUNbMax) ++us;
         const uint32_t nbu = static_cast<uint32_t>(((n2 - 1) >> us) + 1);
         uimg.assign(fast::kDecTableBytes, 0);
-        bool ok = us <= fast::kDecUShiftMax;  // (norm < 3072 * 2^18: s0 below the threshold bits)
+        bool ok = us <= fast::kDecUShiftMax;  // (norm <= 3072 * 2^17: s0 below the threshold bits)
         // threshold word of boundary c in the bucket at a, with s0 in its low bits (ans_fast.hpp
-        // kDecUNbMax): u >= c  <=>  (u - a) << (32 - us) > this word, for u in the bucket
+        // kDecUNbMax): u >= c  <=>  u << (31 - us) > this word (mod 2^32), for u in the bucket:
+        // the shifted u keeps the bucket index's low bit at bit 31, and so does the word, so the
+        // two differ by less than 2^31 and the kernel takes the comparison as the sign of their
+        // difference
         auto word = [&](uint64_t a, uint64_t c, uint32_t s0) {
             const uint64_t rel = std::min<uint64_t>(c - a, 1ull << us);  // >= 1: c > a
-            return static_cast<uint32_t>(((rel - 1) << (32 - us)) | s0);
+            return static_cast<uint32_t>((((a >> us) & 1u) << 31) | ((rel - 1) << (31 - us)) | s0);
         };
         for (uint32_t j = 0; j < nbu && ok; ++j) {
             const uint64_t a = static_cast<uint64_t>(j) << us, end = std::min<uint64_t>(n2, a + (1ull << us));

@@ -95,8 +95,8 @@ def test_random_tables_bit_exact(gpu, nsym, lo, hi, zero_frac, chunk_len, n):
         _roundtrip_vs_oracle(gpu, masses, syms, chunk_len, dtype)
 
 
-@pytest.mark.parametrize("which", ["c3", "c3p2", "wide_masses", "zeros", "top_of_range", "tiny_masses", "shift_19",
-                                   "shift_20"])
+@pytest.mark.parametrize("which", ["c3", "c3p2", "wide_masses", "zeros", "top_of_range", "tiny_masses", "shift_18",
+                                   "shift_19"])
 def test_u_domain_decoder_bit_exact(gpu, which):
     """The fix-up-free decoder (ans_fast.hpp kModeU: u = head - q_m * norm in [0, 2 norm) over a
     512-symbol virtual alphabet) on 256-symbol tables across the fast range: every chunk's bytes
@@ -117,18 +117,19 @@ def test_u_domain_decoder_bit_exact(gpu, which):
         masses = rng.integers(1 << 21, 1 << 23, 256).astype(np.uint64)
         masses = (masses * ((1 << 31) - 1) // int(masses.sum())).astype(np.uint64)
         masses[masses == 0] = 1
-    elif which in ("shift_19", "shift_20"):  # bucket width 2^19 (the widest whose threshold words
-        # leave the 13 row-address bits to s0) and 2^20 (norm above ~8e8: the r02 rows instead)
-        target = 800_000_000 if which == "shift_19" else 900_000_000
+    elif which in ("shift_18", "shift_19"):  # bucket width 2^18 (the widest whose threshold words,
+        # below 2^31 since r06, leave the 13 row-address bits to s0) and 2^19 (norm above ~4e8:
+        # the r02 rows instead)
+        target = 400_000_000 if which == "shift_18" else 800_000_000
         masses = rng.integers(1 << 20, 1 << 23, 256).astype(np.uint64)
         masses = (masses * target // int(masses.sum())).astype(np.uint64)
     else:  # masses of a few units beside large ones: kmax 4, half-unit points
         masses = np.concatenate([rng.integers(1, 4, 16), rng.integers(1 << 12, 1 << 16, 240)]).astype(np.uint64)
     assert int(masses.sum()) < (1 << 31)
     gt = A.GpuTable(gpu, A.Categorical(masses))
-    if which in ("c3", "c3p2", "shift_19"):  # (random tables may hold crowded buckets: kModeFar / kModeRows)
+    if which in ("c3", "c3p2", "shift_18"):  # (random tables may hold crowded buckets: kModeFar / kModeRows)
         assert gt.paths() & A.ANS_PATH_DEC_U, hex(gt.paths())
-    if which == "shift_20":
+    if which == "shift_19":
         assert not gt.paths() & A.ANS_PATH_DEC_U, hex(gt.paths())
     n = 300 * 4096 + 777
     syms = orc.gen_iid(masses, 5, 0, n)
