@@ -35,10 +35,11 @@ constexpr int kRingDwords = 32;  // 128-byte ring per lane = 2 pages of 64 bytes
 constexpr int kGroupBytes = 64;  // symbols move in 64-byte groups (4 units)
 // encode LDS rows: rcp[257], (mass, cum)[257] and the first renorm threshold
 // thr[257] = p*K*2^8 - 1 (saturated at 2^64 - 1); the others follow from it (k_encode)
-// LDS-row encoder tables at offset 0: rcp (8 B per symbol) at 0, then 16-B rows
-// {mass, cum, renorm word} at kEncRowOffset (row of symbol s at kEncRowOffset + 16 s)
+// LDS-row encoder tables at offset 0, three 8-B arrays indexed by 8 s: rcp at 0, {mass, cum} at
+// kEncRowOffset, the renorm word at kEncThrOffset (one address per symbol for all three reads)
 constexpr uint32_t kEncRowOffset = (8 * 257 + 15) & ~15u;
-constexpr uint32_t kEncLdsBytes = kEncRowOffset + 16 * 257;
+constexpr uint32_t kEncThrOffset = kEncRowOffset + ((8 * 257 + 15) & ~15u);
+constexpr uint32_t kEncLdsBytes = kEncThrOffset + 8 * 257;
 constexpr uint32_t kEncRingBytes = kRingDwords * kBlock * 4;  // 64 KiB
 // encode LDS: the row tables at offset 0 (a row address is the symbol times 8, each array at an
 // immediate offset), the ring after them at a multiple of 256 B (the ds_write2st64 offset unit),
@@ -408,13 +409,15 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
     static_assert(kNR != kNormBig || !kGlobalRows, "2^31 < norm: the large-alphabet rows take k_encode_w");
     static_assert(!kM24 || (!kGlobalRows && kNR == kNormStd), "kM24: the LDS rows of the standard range");
     extern __shared__ __align__(16) unsigned char lds[];
-    // a symbol's row is two random LDS reads: rcp by ds_read_b64 (32-lane groups over 32 bank
-    // pairs) and {mass, cum, renorm word} by one ds_read_b128 (16-lane groups over 16 bank
-    // quads).  Three 8-B arrays read by three ds_read_b64 cost ~1.1x the LDS cycles for random
-    // rows (expected worst bank load 3.9 of 32 lanes vs 3.3 of 16) and one more instruction.
+    // a symbol's row is three random ds_read_b64 (32-lane groups over 32 bank pairs) from 8-B
+    // arrays at one address, 8 s: rcp, {mass, cum} and the renorm word.  r06: against rcp by
+    // ds_read_b64 and {mass, cum, renorm word} by one ds_read_b128 (16-lane groups over 16 bank
+    // quads, ~7% fewer conflict cycles), one VALU less per push (the 16-B row's address), the
+    // encoder being VALU-issue bound (0.92 of the issue slots, profiles/r06g_pmc_c3.json).
     // Tables at offset 0, ring after them (kEncRingBase)
     double* rcps = reinterpret_cast<double*>(lds);
-    uint4* rows = reinterpret_cast<uint4*>(lds + kEncRowOffset);
+    uint2* rows = reinterpret_cast<uint2*>(lds + kEncRowOffset);
+    uint2* thrs = reinterpret_cast<uint2*>(lds + kEncThrOffset);
     // u8 symbols index the rows unclamped: all 256 byte values get a row (zero mass beyond the
     // alphabet, so they fail like the sentinel row they used to be clamped to)
     constexpr bool kByteRows = sizeof(Sym) == 1;
@@ -423,11 +426,13 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         for (uint32_t i = threadIdx.x; i < nrows; i += kBlock) {
             const EncRow r = i < t.enc_rows ? t.enc[i] : EncRow{0.0, 0u, 0u};
             const uint64_t w = enc_thr(static_cast<uint64_t>(r.mass) * t.K, t.L);
-            if constexpr (kM24) {  // {mass | 8 k0 << 24, cum, T - 1} (T's low byte is zero)
+            if constexpr (kM24) {  // {mass | 8 k0 << 24, cum}, T - 1 (T's low byte is zero)
                 const uint64_t tm1 = (w & ~0xFFull) - 1u;
-                rows[i] = make_uint4(r.mass | (lo32(w) << 24), r.cum, lo32(tm1), hi32(tm1));
+                rows[i] = make_uint2(r.mass | (lo32(w) << 24), r.cum);
+                thrs[i] = make_uint2(lo32(tm1), hi32(tm1));
             } else {
-                rows[i] = make_uint4(r.mass, r.cum, lo32(w), hi32(w));
+                rows[i] = make_uint2(r.mass, r.cum);
+                thrs[i] = make_uint2(lo32(w), hi32(w));
             }
             rcps[i] = r.rcp;  // 0 for zero mass: such a push always takes the voted branch
         }
@@ -438,10 +443,10 @@ __global__ __launch_bounds__(kBlock, kGlobalRows ? 2 : 4) void k_encode(FastTabl
         uint64_t thr;
     };
     auto row_at = [&](uint32_t off) __attribute__((always_inline)) {  // off = 8 * symbol (tables at LDS offset 0)
-        const uint4 v = lds_ld128(shl16<1>(off) + kEncRowOffset);  // 16 * symbol < 2^16
+        const uint64_t v = lds_ld64(off + kEncRowOffset), w = lds_ld64(off + kEncThrOffset);
         Row r;
-        r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), v.x, v.y};
-        r.thr = mk64(v.w, v.z);
+        r.e = EncRow{__longlong_as_double(static_cast<long long>(lds_ld64(off))), lo32(v), hi32(v)};
+        r.thr = w;
         return r;
     };
     const Ring ring{4 * threadIdx.x};

@@ -396,7 +396,7 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     ft.dec_global = !ft.dec_usable;
     // compact 16-B buckets for k_decode_w: the finest width with at most 2^17 buckets (2 MiB),
     // if every bucket's five candidate offsets fit u16
-    std::vector<DecBucketC> decc;
+    std::vector<DecBucketC> decc, decl;
     if (ft.dec_global) {
         uint32_t cs = 0;
         while (((static_cast<uint64_t>(t.norm) - 1) >> cs) + 1 > (1ull << 17)) ++cs;
@@ -417,8 +417,39 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
         if (fits) {
             ft.dec_c = 1;
             ft.dec_c_shift = cs;
+            ft.dec_cl_shift = cs;
         } else {
             decc.clear();
+        }
+        // the LDS beside k_decode_w's ring holds kWideDecBktLds buckets; a table with more stages
+        // its first ones at twice the width, which doubles the share of lookups the LDS serves
+        // (C4: 9.2% -> 18.3%), if they resolve among their five candidates for all but 1/256 of
+        // the cf they cover (C4: 0.23%; the rest re-fetch their global bucket, ans_wide.hpp)
+        if (ft.dec_c && ncb > fast::kWideDecBktLds) {
+            const uint32_t ls = cs + 1;
+            const uint32_t nl = static_cast<uint32_t>(std::min<uint64_t>(((static_cast<uint64_t>(t.norm) - 1) >> ls) + 1,
+                                                                         fast::kWideDecBktLds));
+            decl.resize(nl);
+            bool lfits = true;
+            uint64_t far = 0, covered = 0;
+            for (uint32_t j = 0; j < nl && lfits; ++j) {
+                const uint64_t b0 = static_cast<uint64_t>(j) << ls;
+                const uint64_t b1 = std::min<uint64_t>(b0 + (1ull << ls), t.norm);
+                const uint32_t s0 = static_cast<uint32_t>(cat.icdf(b0).first);
+                DecBucketC& d = decl[j];
+                d.c0 = cum[s0];
+                d.s0 = static_cast<uint16_t>(s0);
+                for (int k = 0; k < 5; ++k) {
+                    const uint32_t off = cum[s0 + 1 + k] - cum[s0];
+                    if (off > 0xFFFFu) lfits = false;
+                    d.d[k] = static_cast<uint16_t>(off);
+                }
+                const uint64_t c5 = std::max<uint64_t>(cum[s0 + 5], b0);
+                far += b1 > c5 ? b1 - c5 : 0;
+                covered += b1 - b0;
+            }
+            if (lfits && far * 256 <= covered) ft.dec_cl_shift = ls;
+            else decl.clear();
         }
     }
     ft.enc_wide = ft.enc_global && t.norm >= fast::kWideNormMin;
@@ -551,7 +582,9 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     const size_t ws0_b = sizeof(uint16_t) * wide_s0.size();
     const size_t o_decc = o_ws0 + ((ws0_b + 255) & ~size_t(255));
     const size_t decc_b = sizeof(DecBucketC) * decc.size();
-    const size_t o_pack = o_decc + ((decc_b + 255) & ~size_t(255));
+    const size_t o_decl = o_decc + ((decc_b + 255) & ~size_t(255));
+    const size_t decl_b = sizeof(DecBucketC) * decl.size();
+    const size_t o_pack = o_decl + ((decl_b + 255) & ~size_t(255));
     const size_t pack_b = sizeof(uint32_t) * pack_img.size();
     const size_t o_sa = o_pack + ((pack_b + 255) & ~size_t(255));
     const size_t o_grow = o_sa + ((sa_img.size() + 255) & ~size_t(255));
@@ -576,6 +609,8 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     if (ws0_b) HIP_TRY(hipMemcpy(base + o_ws0, wide_s0.data(), ws0_b, hipMemcpyHostToDevice));
     if (decc_b) HIP_TRY(hipMemcpy(base + o_decc, decc.data(), decc_b, hipMemcpyHostToDevice));
     ft.dbkt_c = reinterpret_cast<const DecBucketC*>(base + o_decc);
+    if (decl_b) HIP_TRY(hipMemcpy(base + o_decl, decl.data(), decl_b, hipMemcpyHostToDevice));
+    ft.dbkt_cl = decl_b ? reinterpret_cast<const DecBucketC*>(base + o_decl) : ft.dbkt_c;
     if (pack_b) HIP_TRY(hipMemcpy(base + o_pack, pack_img.data(), pack_b, hipMemcpyHostToDevice));
     ft.enc_pack_img = reinterpret_cast<const uint32_t*>(base + o_pack);
     if (!sa_img.empty()) HIP_TRY(hipMemcpy(base + o_sa, sa_img.data(), sa_img.size(), hipMemcpyHostToDevice));

@@ -310,7 +310,7 @@ inline size_t wide_enc_lds(const FastTable& ft) {
 // in 8.55 ms staged vs 8.98 ms (profiles/r05_ab_c4_2e31_two_wg_per_cu_rejected.txt; a C4 shard,
 // 256 workgroups, is the same either way): the L2 request rate, not the wave count, binds.
 inline size_t wide_dec_lds(FastTable& ft, unsigned /*wgrid*/, int /*ncu*/) {
-    const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(ft.norm) - 1) >> ft.dec_c_shift) + 1);
+    const uint32_t nb = static_cast<uint32_t>(((static_cast<uint64_t>(ft.norm) - 1) >> ft.dec_cl_shift) + 1);
     ft.dec_c_nlb = std::min(nb, fast::kWideDecBktLds);
     return fast::kWideDecTab + 16ull * ft.dec_c_nlb;
 }

@@ -133,6 +133,10 @@ struct FastTable {
     uint32_t dec_c;
     uint32_t dec_c_shift;
     uint32_t dec_c_nlb;  // k_decode_w<kCompact, !kPrefix>: the first buckets staged in LDS (set per launch)
+    // ... staged from dbkt_cl, buckets of width 2^dec_cl_shift: dbkt_c itself, or (tables with more
+    // buckets than the LDS holds) the first kWideDecBktLds buckets at twice dbkt_c's width
+    const DecBucketC* dbkt_cl;
+    uint32_t dec_cl_shift;
     // k_decode kModeU (ans_fast.hpp): the quotient from below without a fix-up; u = head - q_m*norm
     // in [0, 2 norm) indexes a virtual 512-symbol alphabet whose buckets (width 2^dec_u_shift)
     // all resolve among three candidates.  dec_u_img is the LDS image (fast::kDecTableBytes).

@@ -544,9 +544,12 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
     // the LDS the ring leaves (up to kWideDecBktLds: 6,016 of C4's 65,704), so that share of the
     // lookups issues no L2 request (the decoder runs at ~0.87 of the L2 gather ceiling, DESIGN.md
     // §3.3).  The launcher sizes the dynamic LDS for them (ans_launch_impl.hpp wide_dec_lds).
+    // Tables with more buckets than that stage theirs at twice the width (t.dbkt_cl, shift
+    // dec_cl_shift = dec_c_shift + 1: C4 9.2% -> 18.3% of lookups); the 1/256 or less of a staged
+    // bucket's cf beyond its five candidates re-fetches the lane's global bucket (far below).
     const uint32_t nlb = kCompact && !kPrefix ? t.dec_c_nlb : 0u;
     if constexpr (kCompact && !kPrefix) {
-        const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt_c);
+        const uint4* gb = reinterpret_cast<const uint4*>(t.dbkt_cl);
         uint4* lb = reinterpret_cast<uint4*>(lds + kWideDecTab);
         for (uint32_t i = threadIdx.x; i < nlb; i += kWideDecLanes) lb[i] = gb[i];
     }
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
     const uint32_t lcum = kWideDecTab + t.dec_w_cum_off;  // LDS byte address of cdf(0)
     const DecBucketG* __restrict__ bkt = t.dbkt_g;
     const DecBucketC* __restrict__ bktc = t.dbkt_c;
-    const uint32_t cshift = t.dec_c_shift;
+    const uint32_t cshift = t.dec_c_shift, clshift = t.dec_cl_shift;
     const uint32_t* __restrict__ gcum = t.cum;
     uint4* dst = reinterpret_cast<uint4*>(out + c * chunk_len);
 
@@ -579,6 +582,25 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
     ch.col = 4 * threadIdx.x;
     ch.start(slots + (offsets ? offsets[c] : c * slot_cap), static_cast<int32_t>(lens[c]));
     ch.pull_until(L);  // Message::unflatten: head 0, renorm_up pulls the flushed head
+
+    // a compact bucket (c0 | s0, d0 | d1, d2 | d3, d4) resolved for cf: the pop's p = pmf(s), r = cf -
+    // cdf(s) and s among s0 .. s0 + 4 (src/codec.rs:65-68); far: cf lies past the five candidates
+    auto resolve_c = [](const uint4& g, uint32_t cf, uint32_t& p, uint32_t& r, uint32_t& sx, bool& far)
+        __attribute__((always_inline)) {
+        const uint32_t rel = cf - g.x;  // cf - cdf(s0); the candidates' offsets are cdf - cdf(s0)
+        const uint32_t d0 = g.y >> 16, d1 = g.z & 0xFFFFu, d2 = g.z >> 16, d3 = g.w & 0xFFFFu, d4 = g.w >> 16;
+        const bool b1 = rel >= d0, b2 = rel >= d1, b3 = rel >= d2, b4 = rel >= d3;
+        // (lo, hi) = (d_{k-1}, d_k) as ONE packed word, selected among the five consecutive
+        // 16-bit pairs of the sequence 0, d0, .., d4 (two of them funnelled by v_alignbit):
+        // four selects where two chains of four selected lo and hi apart (r05)
+        const uint32_t w1 = __builtin_amdgcn_alignbit(g.z, g.y, 16u);  // d0 | d1
+        const uint32_t w3 = __builtin_amdgcn_alignbit(g.w, g.z, 16u);  // d2 | d3
+        const uint32_t pr = b4 ? g.w : (b3 ? w3 : (b2 ? g.z : (b1 ? w1 : (g.y & 0xFFFF0000u))));
+        p = (pr >> 16) - (pr & 0xFFFFu);
+        r = rel - (pr & 0xFFFFu);
+        sx = (g.y & 0xFFFFu) + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
+        far = rel >= d4;
+    };
 
     auto step = [&]() __attribute__((always_inline)) {
         // the chain's part up to the bucket loads at raised wave priority (ans_fast.hpp k_decode;
@@ -594,10 +616,10 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
                 // one load per lane into the same registers, L2 or LDS under complementary exec
                 // masks (r05: the LDS read on every lane and a 4-dword select added 12 VALU per
                 // symbol to the r04 decoder)
-                const uint32_t bi = cf >> cshift;
-                const uint4* gp = reinterpret_cast<const uint4*>(bktc + bi);  // c0 | s0, d0 | d1, d2 | d3, d4
-                const uint4* lp = reinterpret_cast<const uint4*>(lds + kWideDecTab) + bi;  // (generic: the LDS aperture)
-                ga = *(bi < nlb ? lp : gp);
+                const uint32_t bl = cf >> clshift;
+                const uint4* gp = reinterpret_cast<const uint4*>(bktc + (cf >> cshift));  // c0 | s0, d0 | d1, d2 | d3, d4
+                const uint4* lp = reinterpret_cast<const uint4*>(lds + kWideDecTab) + bl;  // (generic: the LDS aperture)
+                ga = *(bl < nlb ? lp : gp);
             } else if constexpr (kCompact) {
                 ga = *reinterpret_cast<const uint4*>(bktc + (cf >> cshift));  // c0 | s0, d0 | d1, d2 | d3, d4
             } else {
@@ -629,20 +651,18 @@ __global__ __launch_bounds__(kWideDecLanes, 2) void k_decode_w(FastTable t, cons
             far = cf >= c4;
         } else if constexpr (kCompact) {
             asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w));
-            const uint32_t rel = cf - ga.x;  // cf - cdf(s0); the candidates' offsets are cdf - cdf(s0)
-            const uint32_t d0 = ga.y >> 16, d1 = ga.z & 0xFFFFu, d2 = ga.z >> 16, d3 = ga.w & 0xFFFFu,
-                           d4 = ga.w >> 16;
-            const bool b1 = rel >= d0, b2 = rel >= d1, b3 = rel >= d2, b4 = rel >= d3;
-            // (lo, hi) = (d_{k-1}, d_k) as ONE packed word, selected among the five consecutive
-            // 16-bit pairs of the sequence 0, d0, .., d4 (two of them funnelled by v_alignbit):
-            // four selects where two chains of four selected lo and hi apart (r05)
-            const uint32_t w1 = __builtin_amdgcn_alignbit(ga.z, ga.y, 16u);  // d0 | d1
-            const uint32_t w3 = __builtin_amdgcn_alignbit(ga.w, ga.z, 16u);  // d2 | d3
-            const uint32_t pr = b4 ? ga.w : (b3 ? w3 : (b2 ? ga.z : (b1 ? w1 : (ga.y & 0xFFFF0000u))));
-            p = (pr >> 16) - (pr & 0xFFFFu);
-            r = rel - (pr & 0xFFFFu);
-            sx = (ga.y & 0xFFFFu) + (b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u) + (b4 ? 1u : 0u);
-            far = rel >= d4;
+            if constexpr (!kPrefix) {
+                // lanes past a double-width LDS bucket's five candidates resolve on their global
+                // bucket instead (screened before the resolve, so the step holds one resolve: two
+                // inlined in each of the 64 unrolled steps stopped the unit loop unrolling and put
+                // the symbol lines in scratch, decode +6%)
+                const bool again = cf - ga.x >= (ga.w >> 16) && (cf >> clshift) < nlb && clshift != cshift;
+                if (__builtin_expect(__any(again), 0)) {
+                    if (again) ga = *reinterpret_cast<const uint4*>(bktc + (cf >> cshift));
+                    asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w));
+                }
+            }
+            resolve_c(ga, cf, p, r, sx, far);
         } else {
             asm volatile("" ::"v"(ga.x), "v"(ga.y), "v"(ga.z), "v"(ga.w), "v"(gb.x), "v"(gb.y), "v"(gb.z));
             const bool b1 = cf >= ga.y, b2 = cf >= ga.z, b3 = cf >= ga.w, b4 = cf >= gb.x;

@@ -1,19 +1,14 @@
-# Same-box A/B of two library builds (tools/inproc_ab.py) on C3, C4 and the C3 dense container;
-# then B becomes the in-tree library on the box (a scratch copy) and the GPU test suite and the
-# default bench line run on it (tools/gpu_step.sh).
-# usage: bash tools/gpu_ab.sh <libdir A> <libdir B>      (libdirs under shuffle-coding_amd/)
+# Same-box A/B of the current build against lib_base: the parity tests named in AB_TESTS first
+# (default: the C3/C4 parity and norm-range suites), then tools/inproc_ab.py in both orders with
+# the caller's AB_CONFIG / AB_LOG2N.   usage: AB_CONFIG=c4 AB_LOG2N=29 bash tools/gpu_ab.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-run() {  # tag, env..., iters
-    local tag=$1; shift
-    env "$@" timeout -k 10 300 python -u tools/inproc_ab.py $A $B ${ITERS:-40} > gpurun_out/ab_$tag.txt 2>&1
-    local rc=$?; echo "ab $tag rc=$rc"; grep -v amdgpu.ids gpurun_out/ab_$tag.txt; return $rc
-}
-A=$1; B=$2
-run c3 AB_CONFIG=c3 || exit $?
-ITERS=20 run c4 AB_CONFIG=c4 || exit $?
-run dense AB_CONFIG=c3 AB_DENSE=1 || exit $?
-if [ "$B" != lib ]; then cp shuffle-coding_amd/$B/libshufflecoding_amd.so shuffle-coding_amd/lib/; fi
-bash tools/gpu_step.sh || exit $?
+TAG=${1:-ab}
+TESTS=${AB_TESTS:-tests/test_gpu_parity.py tests/test_gpu_norm_ranges.py}
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu $TESTS > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/inproc_ab.py lib_base lib ${ITERS:-30} > gpurun_out/${TAG}_ab.txt 2>&1
+rc=$?; echo "ab rc=$rc"; grep -v amdgpu.ids gpurun_out/${TAG}_ab.txt | tail -6; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/inproc_ab.py lib lib_base ${ITERS:-30} > gpurun_out/${TAG}_ab_rev.txt 2>&1
+rc=$?; echo "ab rev rc=$rc"; grep -v amdgpu.ids gpurun_out/${TAG}_ab_rev.txt | tail -6
