@@ -363,26 +363,43 @@ def c4_pass(ctx, args):
     names =(kernel_name(A, gt, "encode", sym_bytes), kernel_name(A, gt, "decode", sym_bytes))
     del syms, slots, lens, out
     torch.cuda.empty_cache()
-    return [elapsed, enc_ms, dec_ms, comp, bad], names, n, int(masses.sum())
+    return [elapsed, enc_ms, dec_ms, comp, bad], names, n, masses
 
 
-def c4_l2_share(norm):
-    """The share of k_decode_w's bucket lookups that go to L2: its compact buckets have the finest
-    width with at most 2^17 of them (ans_kernels.hip build_fast_table), and the first
-    kWideDecBktLds = (160 KiB - 67,584 B of ring) / 16 = 6,016 are read from LDS (ans_wide.hpp);
-    cf is uniform over the buckets."""
+def c4_l2_share(masses):
+    """The share of k_decode_w's bucket lookups that go to L2.  Its compact buckets have the finest
+    width 2^cs with at most 2^17 of them (ans_kernels.hip build_fast_table); kWideDecBktLds =
+    (160 KiB - 67,584 B of ring) / 16 = 6,016 buckets fit in LDS (ans_wide.hpp), staged at width
+    2^(cs+1) when the table has more buckets and at most 1/256 of the staged cf lies past a staged
+    bucket's five candidates (such lookups re-fetch their global bucket); cf is uniform."""
+    m = np.asarray(masses, dtype=np.int64)
+    cum = np.concatenate([[0], np.cumsum(m), np.full(5, m.sum())])
+    norm = int(cum[len(m)])
+    nlds = (160 * 1024 - 67584) // 16
     cs = 0
     while ((norm - 1) >> cs) + 1 > (1 << 17):
         cs += 1
     nb = ((norm - 1) >> cs) + 1
-    return 1.0 - min(nb, (160 * 1024 - 67584) // 16) / nb
+    if nb <= nlds:
+        return 0.0
+    ls = cs + 1
+    nl = min(((norm - 1) >> ls) + 1, nlds)
+    b0 = np.arange(nl, dtype=np.int64) << ls
+    b1 = np.minimum(b0 + (1 << ls), norm)
+    s0 = np.searchsorted(cum[:len(m) + 1], b0, side="right") - 1
+    far = np.maximum(0, b1 - np.maximum(cum[s0 + 5], b0)).sum()
+    covered = int((b1 - b0).sum())
+    if far * 256 > covered:
+        ls, covered, far = cs, min(nlds << cs, norm), 0
+    return 1.0 - (covered - far) / norm
 
 
-def c4_summary(rows, names, n, norm, args, world):
+def c4_summary(rows, names, n, masses, args, world):
     """The c4 sub-object from every rank's [elapsed, enc_ms, dec_ms, comp, bad]."""
     sym_bytes = 2
     wall = max(r[0] for r in rows)
-    share = c4_l2_share(norm)
+    share = c4_l2_share(masses)
+    norm = int(np.asarray(masses, dtype=np.int64).sum())
     per = []
     for r in rows:
         alg = n * sym_bytes + r[3]
@@ -581,7 +598,7 @@ def main():
 
     c4, c4_row = None, None
     if args.config != "c4" and not args.no_c4:
-        c4_row, c4_names, c4_n, c4_norm = c4_pass(ctx, args)  # [elapsed, enc_ms, dec_ms, comp, bad]
+        c4_row, c4_names, c4_n, c4_masses = c4_pass(ctx, args)  # [elapsed, enc_ms, dec_ms, comp, bad]
 
     # every rank's [elapsed, bad, enc_ms, dec_ms, n, comp_bytes] (+ its c4 row)
     rows = ctx.gather([elapsed, bad, enc_ms, dec_ms, float(n), float(comp_bytes)] + (c4_row or []))
@@ -589,7 +606,7 @@ def main():
         msg = A.lib().ans_status_string(st).decode() if st else "decoded symbols differ (this or another rank)"
         raise SystemExit(f"rank {rank}: round trip failed ({msg})")
     if c4_row is not None:
-        c4 = c4_summary([r[6:] for r in rows], c4_names, c4_n, c4_norm, args, world)
+        c4 = c4_summary([r[6:] for r in rows], c4_names, c4_n, c4_masses, args, world)
 
     host = None
     if world == 1 and not args.no_host and args.config in ("c3", "c3p2", "c3s", "c3b"):
