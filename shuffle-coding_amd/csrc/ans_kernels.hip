@@ -498,12 +498,17 @@ int build_fast_table(ans_gpu_table* gt, const Categorical& cat) {
     }
     if (!ft.enc_sa) sa_img.clear();
     // the packed encoder's global rows (ans_table.hpp enc_grow): (cdf(s), O(s) | O(s+1) << 16)
+    // k_encode_w reads the global row of every symbol, the prefix's lanes at row nl - 1 (zero), and
+    // every symbol's LDS row at min(s, nl), which for s >= nl is row C = (cdf(nl), O(nl) | O(nl+1)
+    // << 16); it XORs the two, so the global rows from nl on are stored XORed with C
     std::vector<uint32_t> grow;
     if (ft.enc_pack) {
+        const uint32_t nl = ft.enc_nl;
         grow.resize(2 * (static_cast<size_t>(nsym) + 1));
+        const uint32_t c0 = cum[nl], c1 = (cum[nl] & 0xFFFFu) | (cum[nl + 1] << 16);
         for (uint32_t k = 0; k <= nsym; ++k) {
-            grow[2 * k] = cum[k];
-            grow[2 * k + 1] = (cum[k] & 0xFFFFu) | (cum[k + 1] << 16);
+            grow[2 * k] = k >= nl ? cum[k] ^ c0 : 0u;
+            grow[2 * k + 1] = k >= nl ? ((cum[k] & 0xFFFFu) | (cum[k + 1] << 16)) ^ c1 : 0u;
         }
     }
     // k_decode_w's LDS prefix: for each bucket width 2^shp, the longest prefix of symbols whose

@@ -56,6 +56,7 @@ static_assert(WideEncLds<true, true>::cum + ((2u * (wide_pack_nl_max(true) + 2u)
 typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 
 // (cdf(s), cdf(s+1)) from the global cdf array: one 8-B load at a 4-B aligned address
 __device__ __forceinline__ v2u32 cum_pair_global(const uint32_t* cum, uint32_t s) {
@@ -172,6 +173,16 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
     // Packed rows: (B, O(s) | O(s+1) << 16), the two low halves in one register (lrow reads
     // them by halves; as separate u32 values each took a v_and).
     using LRow = v2u32;
+    // kPack: the global rows load on every lane, into their own registers, with no exec mask: a
+    // lane in the prefix reads row nl - 1, all zero, and a lane past it the row XORed with its
+    // LDS read C = row nl (FastTable::enc_grow), so lbuf ^ gbuf is the symbol's row either way
+    auto request_g = [&](const uint4& unit, LRow* gbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
+            gbuf[j] = cum_pair_global(t.enc_grow, 2 * umax(s, nl - 1));
+        }
+    };
     auto request = [&](const uint4& unit, LRow* lbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -189,10 +200,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
                 lbuf[j] = cum_pair_lds(Lay::cum, sp);
             }
         }
+        if constexpr (!kPack) {
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
-            if (s >= nl) lbuf[j] = kPack ? cum_pair_global(t.enc_grow, 2 * s) : cum_pair_global(gcum, s);
+            for (int j = 0; j < U; ++j) {
+                const uint32_t s = umin(sym_of<Sym>(unit, j), nsym);
+                if (s >= nl) lbuf[j] = cum_pair_global(gcum, s);
+            }
         }
     };
     // (cdf(s), pmf(s)) of a symbol.  Packed (ans_kernels.hip build_fast_table): B = cdf(16 b) of
@@ -230,14 +243,18 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         return (head >> m8) >= pK ? m8 : m8 - 8u;
     };
     // the row of symbol j of a unit: cdf(x), pmf(x) (src/codec.rs:63-64)
-    auto process = [&](const LRow* lbuf, uint32_t upos) __attribute__((always_inline)) {
+    auto process = [&](const LRow* lbuf, const LRow* gbuf, uint32_t upos) __attribute__((always_inline)) {
+        auto row_of = [&](int j) __attribute__((always_inline)) {
+            if constexpr (kPack) return lrow(lbuf[j] ^ gbuf[j]);
+            else return lrow(lbuf[j]);
+        };
         // kSa: the unit's rows and shift bytes first (p <= kWideSaMax: the byte at LDS address p)
         v2u32 rows[U];
         uint32_t sas[U];
         if constexpr (kSa) {
 #pragma unroll
             for (int j = U - 1; j >= 0; --j) {
-                rows[j] = lrow(lbuf[j]);
+                rows[j] = row_of(j);
                 sas[j] = *reinterpret_cast<const lds_u8*>(static_cast<uintptr_t>(rows[j].y));
             }
         }
@@ -245,7 +262,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
         for (int j = U - 1; j >= 0; --j) {  // IID::push: last symbol first (src/codec.rs:417)
             if (kVar && upos + j >= nvalid) continue;  // past the chunk (its first, partial group)
             __builtin_amdgcn_s_setprio(2);  // the push at raised wave priority (encode -0.4%, A/B)
-            const v2u32 row = kSa ? rows[j] : lrow(lbuf[j]);
+            const v2u32 row = kSa ? rows[j] : row_of(j);
             const uint32_t cum = row.x, p = row.y;
             const uint64_t pK = kK32 ? static_cast<uint64_t>(p) * static_cast<uint32_t>(K) : static_cast<uint64_t>(p) * K;
             uint32_t k8;
@@ -295,9 +312,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
 #pragma unroll
         for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
     }
-    LRow la[U], lb[U];
+    // r06: the packed rows' global loads on every lane (request_g) measured encode -1.2/-2.3% in a
+    // same-box A/B against the exec-masked loads; requesting them TWO units ahead with the
+    // compiler's own vmcnt waits instead of the points' (four rotating sets) +2.2%
+    // (profiles/r06l_ab_c4_enc_two_ahead_rejected.txt)
+    LRow la[U], lb[U], ga[U], gb[U];
     wait_vm();
     request(n[GU - 1], la);
+    if constexpr (kPack) request_g(n[GU - 1], ga);
     for (int g = ngroups - 1; g >= 0; --g) {
         uint4 cc[GU];
 #pragma unroll
@@ -310,14 +332,20 @@ __global__ __launch_bounds__(kBlock, 2) void k_encode_w(FastTable t, const Sym* 
             else wait_vm();
             flush();
             const bool odd = (u & 1) != 0;
-            if (u > 0) request(cc[u - 1], odd ? lb : la);
+            if (u > 0) {
+                request(cc[u - 1], odd ? lb : la);
+                if constexpr (kPack) request_g(cc[u - 1], odd ? gb : ga);
+            }
             if (u == GU - 1 && g > 0) {
                 const uint4* gsrc = src + GU * (g - 1);
 #pragma unroll
                 for (int i = 0; i < GU; ++i) n[i] = gsrc[i];
             }
-            if (u == 0) request(n[GU - 1], la);  // unit GU-1 of group g-1 (landed units ago)
-            process(odd ? la : lb, static_cast<uint32_t>(g * GS + u * U));
+            if (u == 0) {  // unit GU-1 of group g-1 (landed units ago)
+                request(n[GU - 1], la);
+                if constexpr (kPack) request_g(n[GU - 1], ga);
+            }
+            process(odd ? la : lb, odd ? ga : gb, static_cast<uint32_t>(g * GS + u * U));
         }
     }
     wait_vm();
