@@ -100,3 +100,24 @@ def test_bench_eight_ranks_one_device():
     assert abs(d["value"] - 8 * (1 << 20) / (d["ms_per_step"] * 1e-3) / 2**30) < 0.01 * d["value"]
     assert d["c4"]["per_rank"]["ms_per_step"]["max"] == d["c4"]["ms_per_step"]
     assert d["c4"]["workload"].startswith("C4: 2^18 iid u16 symbols per GPU (0.00390625 GiB over 8 GPUs)")
+
+
+def test_c4_l2_share_follows_the_staged_bucket_width():
+    # bench.c4_l2_share restates build_fast_table's rule for k_decode_w's LDS buckets: C4 stages
+    # 6,016 buckets of width 4,096 (twice the global 2,048), so 18.3% of the cf space minus the
+    # 0.23% of it past a staged bucket's five candidates (re-fetched from L2) is served by LDS
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "shuffle-coding_amd"))
+    import numpy as np
+
+    import ans_amd as A
+    import bench
+
+    m = A.c4_masses()
+    norm = int(m.sum())
+    share = bench.c4_l2_share(m)
+    covered = 6016 * 4096
+    assert 1.0 - covered / norm < share < 1.0 - 0.99 * covered / norm
+    assert abs(share - 0.8174) < 1e-3
+    # a table whose buckets all fit in LDS at the fine width serves every lookup from LDS
+    assert bench.c4_l2_share(np.full(300, 20, dtype=np.uint64)) == 0.0  # norm 6,000: 6,000 buckets
