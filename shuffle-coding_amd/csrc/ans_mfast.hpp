@@ -387,9 +387,12 @@ __global__ __launch_bounds__(kL, kL == kLanes ? 2 : 1) void k_menc(Model md, con
                     const uint4& tv = tc[tb / 16];
                     const int wi = (tb % 16) / 4;
                     const uint32_t w = wi == 0 ? tv.x : wi == 1 ? tv.y : wi == 2 ? tv.z : tv.w;
-                    asm volatile("v_bfe_u32 %0, %1, %2, 8" : "=v"(tid) : "v"(w), "i"(8 * (tb % 4)));
+                    // (the low and the top byte by the fast-class v_and / v_lshrrev)
+                    if (tb % 4 == 0) asm volatile("v_and_b32 %0, 0xff, %1" : "=v"(tid) : "v"(w));
+                    else if (tb % 4 == 3) asm volatile("v_lshrrev_b32 %0, 24, %1" : "=v"(tid) : "v"(w));
+                    else asm volatile("v_bfe_u32 %0, %1, %2, 8" : "=v"(tid) : "v"(w), "i"(8 * (tb % 4)));
                 }
-                md.push(e, lo, hi, tid);
+                md.template push<decltype(e), sizeof(Sym) == 1>(e, lo, hi, tid);
             }
         };
         unroll_seq(unit, std::make_integer_sequence<int, GU>{});
@@ -841,9 +844,10 @@ struct IndepModel {
     __device__ __forceinline__ void stage_dec(unsigned char* l, uint32_t nl) const { stage_image(dec_img, dec_bytes, l, nl); }
 
     // blanket push (src/ans.rs:96-105) with Categorical t's row (src/codec.rs:63-64)
-    template <class E>
+    // kByte: u8 symbols, below 256 already (no clamp to the sentinel row: -1 VALU per push)
+    template <class E, bool kByte = false>
     __device__ __forceinline__ void push(E& e, uint32_t sym, uint32_t, uint32_t tid) const {
-        const uint32_t i = __umul24(tid, 257u) + min(sym, 256u);  // row 257 t + s
+        const uint32_t i = __umul24(tid, 257u) + (kByte ? sym : min(sym, 256u));  // row 257 t + s
         const uint4 r = lds_ld128(kTabE + shl16<4>(i));          // {p, cdf, w}
         uint32_t ra, na;
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ra) : "v"(i), "s"(ro));
@@ -1037,7 +1041,7 @@ struct UniformModel {
 
     __device__ __forceinline__ void stage_enc(unsigned char*, uint32_t) const {}
     __device__ __forceinline__ void stage_dec(unsigned char*, uint32_t) const {}
-    template <class E>
+    template <class E, bool kByte = false>
     __device__ __forceinline__ void push(E& e, uint32_t lo, uint32_t hi, uint32_t) const {
         const uint64_t x = mk64(hi, lo);
         if (x >= size) e.err |= kErrSymbol;  // outside the alphabet (the reference would code garbage)
@@ -1087,7 +1091,7 @@ struct LogUniformModel {
 
     __device__ __forceinline__ void stage_enc(unsigned char*, uint32_t) const {}
     __device__ __forceinline__ void stage_dec(unsigned char*, uint32_t) const {}
-    template <class E>
+    template <class E, bool kByte = false>
     __device__ __forceinline__ void push(E& e, uint32_t lo, uint32_t hi, uint32_t) const {
         const uint64_t x = mk64(hi, lo);
         const uint32_t bits = x ? 64u - static_cast<uint32_t>(__builtin_clzll(x)) : 0u;  // LogUniform::get_bits

@@ -14,6 +14,6 @@ for cfg in "$@"; do
   if [ "$name" = c3 ]; then unset AB_CONFIG AB_LOG2N; else export AB_CONFIG=$name; [ "$n" != "$cfg" ] && export AB_LOG2N=$n; fi
   for order in "lib_base lib" "lib lib_base"; do
     timeout -k 10 300 python -u tools/inproc_ab.py $order ${ITERS:-30} > gpurun_out/${TAG}_ab_${name}.txt 2>&1
-    rc=$?; echo "== $name ($order) rc=$rc"; grep -v amdgpu.ids gpurun_out/${TAG}_ab_${name}.txt | tail -2; [ $rc -eq 0 ] || exit $rc
+    rc=$?; echo "== $name ($order) rc=$rc"; grep -v amdgpu.ids gpurun_out/${TAG}_ab_${name}.txt | tail -3; [ $rc -eq 0 ] || exit $rc
   done
 done
